@@ -1,0 +1,201 @@
+"""Deterministic solver-level inputs for the parity fixtures.
+
+Test infrastructure only. Every tensor is built from the five TUM fr1/desk
+example frames the reference ships (`code/data/data_examples/TUM`, stored here
+as `tum_fr1_desk_frames.npz`) with exactly-rounded IEEE ops only (+, -, *, /,
+floor, abs, min/max, clip), so the same bits come out on any host with the
+same numpy.  SHA-256 digests of every tensor are stored beside the golden
+outputs and re-checked before a comparison.
+
+The trained checkpoints are absent (`.MISSING_LARGE_BLOBS:1-2` in the
+reference), so features are a synthetic stand-in: C triangle-wave transforms
+of the grey image at level l, and one uncertainty channel clipped to
+[SIGMA_LO, SIGMA_HI] so that many pixels sit exactly at the batch-global
+min / max (this exercises the truncated-sigma mask of
+`code/models/algorithms.py:1975-1980`).
+
+Inverse depth follows `LeastSquareTracking._preprocess`
+(`code/models/LeastSquareTracking.py:656-661`): clamp(1/depth, 0, 10) then the
+batch-global min and max are zeroed; pyramids are max-pools of level 0
+(`algorithms.py:1201-1219`), depth is read as uint16/5000 clipped to [0.5, 5]
+(`code/data/SimpleLoader.py:77-80`).
+"""
+import hashlib
+import os
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+FRAMES = os.path.join(HERE, "tum_fr1_desk_frames.npz")
+K_FULL = np.array([525.0, 525.0, 319.5, 239.5], dtype=np.float32)  # code/test.py:68
+SIGMA_LO, SIGMA_HI = np.float32(0.5), np.float32(1.5)
+
+_frames_cache = {}
+
+
+def frames():
+    if "f" not in _frames_cache:
+        z = np.load(FRAMES, allow_pickle=False)
+        _frames_cache["f"] = (z["color"], z["depth"])
+    return _frames_cache["f"]
+
+
+def _pool_sum(a, k):
+    """k x k sum pooling of an integer array (exact)."""
+    if k == 1:
+        return a.astype(np.int64)
+    H, W = a.shape[-2:]
+    a = a.astype(np.int64).reshape(a.shape[:-2] + (H // k, k, W // k, k))
+    return a.sum(axis=(-1, -3))
+
+
+def _tri(x):
+    """Triangle wave in [0, 1]: |2 (x - floor(x + 1/2))| -- exactly-rounded ops only."""
+    x = x.astype(np.float32)
+    return np.abs(np.float32(2.0) * (x - np.floor(x + np.float32(0.5)))).astype(np.float32)
+
+
+def grey_int(idx, base_down=1):
+    """Integer grey image (77R + 150G + 29B), optionally sum-pooled to a lower base."""
+    color, _ = frames()
+    c = color[idx].astype(np.int64)
+    g = 77 * c[..., 0] + 150 * c[..., 1] + 29 * c[..., 2]
+    return _pool_sum(g, base_down), base_down * base_down
+
+
+def depth_m(idx, base_down=1):
+    _, depth = frames()
+    d = depth[idx][::base_down, ::base_down].astype(np.float32) / np.float32(5e3)
+    return np.clip(d, np.float32(0.5), np.float32(5.0)).astype(np.float32)
+
+
+def features(idx, C, level, base_down=1):
+    """[C, H_l, W_l] feature stack and [1, H_l, W_l] sigma for frame idx at level."""
+    g, npx = grey_int(idx, base_down)
+    k = 1 << level
+    gs = _pool_sum(g, k)
+    norm = np.float64(65280.0 * npx * k * k)
+    gn = (gs.astype(np.float64) / norm).astype(np.float32)
+    fs = []
+    for c in range(C):
+        freq = np.float32(1.5 + 0.375 * (c % 13))
+        phase = np.float32(c) / np.float32(C)
+        fs.append(_tri(gn * freq + phase))
+    f = np.stack(fs, 0).astype(np.float32)
+    s = np.float32(0.25) + np.float32(1.5) * _tri(gn * np.float32(1.7) + np.float32(0.2))
+    s = np.clip(s, SIGMA_LO, SIGMA_HI).astype(np.float32)[None]
+    return f, s
+
+
+def inv_depth_batch(depths):
+    """`_preprocess` inverse depth for a batch [B,1,H,W] (LeastSquareTracking.py:656-661)."""
+    d = np.stack(depths, 0)[:, None].astype(np.float32)
+    inv = np.clip(np.float32(1.0) / d, np.float32(0), np.float32(10)).astype(np.float32)
+    inv[inv == inv.min()] = 0
+    inv[inv == inv.max()] = 0
+    return inv
+
+
+def max_pool(a, k):
+    if k == 1:
+        return a.copy()
+    B, C, H, W = a.shape
+    return a.reshape(B, C, H // k, k, W // k, k).max(axis=(3, 5))
+
+
+def any_pool(m, k):
+    """ImagePyramids on a bool mask: avg-pool then != 0 (algorithms.py:1214-1216)."""
+    if k == 1:
+        return m.copy()
+    B, C, H, W = m.shape
+    return m.reshape(B, C, H // k, k, W // k, k).any(axis=(3, 5))
+
+
+def so3_exp64(w):
+    w = np.asarray(w, np.float64)
+    th = np.linalg.norm(w)
+    if th == 0:
+        return np.eye(3)
+    k = w / th
+    Kx = np.array([[0, -k[2], k[1]], [k[2], 0, -k[0]], [-k[1], k[0], 0]])
+    return np.eye(3) + np.sin(th) * Kx + (1 - np.cos(th)) * Kx @ Kx
+
+
+def make_case(pairs, C, levels, base_down=1, masks=False, icp=False, init=None):
+    """Build a solver-level case.
+
+    pairs: list of (i, j) frame indices (reference i -> target j)
+    levels: number of pyramid levels (1 = level 0 only)
+    Returns dict with per-level arrays and the initial pose.
+    """
+    B = len(pairs)
+    d0 = [depth_m(i, base_down) for i, _ in pairs]
+    d1 = [depth_m(j, base_down) for _, j in pairs]
+    inv0 = inv_depth_batch(d0)
+    inv1 = inv_depth_batch(d1)
+    dep0 = np.stack(d0, 0)[:, None]
+    dep1 = np.stack(d1, 0)[:, None]
+    K = np.tile((K_FULL / np.float32(base_down))[None], (B, 1)).astype(np.float32)
+    case = {"B": B, "C": C, "levels": levels, "K": K, "pairs": np.array(pairs, np.int32)}
+    if masks:
+        m0 = np.stack([d < np.median(d) for d in d0], 0)[:, None]
+        m1 = np.stack([d < np.median(d) for d in d1], 0)[:, None]
+    for l in range(levels):
+        f0, s0, f1, s1 = [], [], [], []
+        for i, j in pairs:
+            a, sa = features(i, C, l, base_down)
+            b, sb = features(j, C, l, base_down)
+            f0.append(a); s0.append(sa); f1.append(b); s1.append(sb)
+        k = 1 << l
+        case[f"x0_{l}"] = np.stack(f0, 0)
+        case[f"x1_{l}"] = np.stack(f1, 0)
+        case[f"s0_{l}"] = np.stack(s0, 0)
+        case[f"s1_{l}"] = np.stack(s1, 0)
+        case[f"invD0_{l}"] = max_pool(inv0, k)
+        case[f"invD1_{l}"] = max_pool(inv1, k)
+        if icp:
+            case[f"depth0_{l}"] = max_pool(dep0, k)
+            case[f"depth1_{l}"] = max_pool(dep1, k)
+        if masks:
+            case[f"mask0_{l}"] = any_pool(m0, k)
+            case[f"mask1_{l}"] = any_pool(m1, k)
+    if init is None:
+        R = np.tile(np.eye(3, dtype=np.float32)[None], (B, 1, 1))
+        t = np.zeros((B, 3), np.float32)
+    else:
+        R = np.stack([so3_exp64(w) for w, _ in init], 0).astype(np.float32)
+        t = np.stack([np.asarray(tt, np.float64) for _, tt in init], 0).astype(np.float32)
+    case["R_init"] = R
+    case["t_init"] = t
+    return case
+
+
+INPUT_KEYS_PREFIX = ("x0_", "x1_", "s0_", "s1_", "invD0_", "invD1_", "depth0_", "depth1_", "mask0_", "mask1_")
+
+
+def input_digests(case):
+    out = {}
+    for k in sorted(case):
+        if k.startswith(INPUT_KEYS_PREFIX) or k in ("K", "R_init", "t_init"):
+            a = np.ascontiguousarray(case[k])
+            out[k] = hashlib.sha256(a.tobytes()).hexdigest()
+    return out
+
+
+# Named cases shared by the fixture generator and the tests.
+CASES = {
+    # cfg1: frames 0->1, 160x120, C=8, one level, remove_tru_sigma on
+    "cfg1_160x120_c8": dict(pairs=[(0, 1)], C=8, levels=1, base_down=4),
+    # larger motion, 0->4, tru-sigma off
+    "cfg1b_160x120_c8_f04": dict(pairs=[(0, 4)], C=8, levels=1, base_down=4),
+    # batch of 4 pairs, 160x120 C=8 two levels (batch-global masks)
+    "batch4_160x120_c8": dict(pairs=[(0, 1), (1, 2), (2, 3), (0, 4)], C=8, levels=2, base_down=4),
+    # object masks + perturbed init (cfg4 style, small batch)
+    "masks_160x120_c8": dict(pairs=[(0, 2), (3, 1)], C=8, levels=1, base_down=4, masks=True,
+                             init=[([0.01, -0.02, 0.005], [0.02, -0.01, 0.03]),
+                                   ([-0.015, 0.01, 0.0], [-0.03, 0.02, 0.0])]),
+    # joint feature + ICP (cfg5 style) at 160x120
+    "icp_160x120_c8": dict(pairs=[(0, 2)], C=8, levels=2, base_down=4, icp=True),
+    # cfg2: 640x480, C=32, 4 levels
+    "cfg2_640x480_c32": dict(pairs=[(0, 1)], C=32, levels=4, base_down=1),
+}
