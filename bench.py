@@ -1,0 +1,227 @@
+#!/usr/bin/env python
+"""Benchmark: IC solver iterations/s, 640x480, C=32, 4-level pyramid (BASELINE.json).
+
+One *step* = one full coarse-to-fine solve (levels 3..0, 3 Gauss-Newton
+iterations each = 12 IC iterations per pair) of a batch of B frame pairs per
+GPU, replayed from one HIP graph, followed (N > 1) by the RCCL all-gather of
+the per-pair poses.  Workload: cfg3's shard -- B = 8 pairs per GPU cycled from
+the ordered pairs of the five TUM fr1/desk frames, deterministic features
+(tests/golden/recipe.py), inputs resident in HBM before the timed region.
+
+`value` = all-level IC iterations/s over the whole job = N * B * 12 / step time.
+Launch: python bench.py [--gpus N --steps K --warmup W]; for N > 1 under
+torch.distributed.run (one rank per GPU, RCCL).
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+import torch
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+sys.path.insert(0, os.path.join(ROOT, "tests", "golden"))
+
+H0, W0, C, LEVELS, ITERS = 480, 640, 32, 4, 3
+HBM_PEAK_GBS = 8000.0  # MI355X spec, MI355X_MICROARCH.md chip table
+
+
+def parse():
+    p = argparse.ArgumentParser()
+    p.add_argument("--gpus", type=int, default=1)
+    p.add_argument("--steps", type=int, default=20)
+    p.add_argument("--warmup", type=int, default=3)
+    p.add_argument("--batch-per-gpu", type=int, default=8)
+    p.add_argument("--kernel-reps", type=int, default=50)
+    p.add_argument("--no-cpu-baseline", action="store_true")
+    p.add_argument("--no-graph", action="store_true")
+    return p.parse_args()
+
+
+def make_inputs(B, rank, device):
+    import recipe
+    pairs = [(i, j) for i in range(5) for j in range(5) if i != j]
+    sel = [pairs[(rank * B + k) % len(pairs)] for k in range(B)]
+    feat = {}
+
+    def fs(idx, l):
+        if (idx, l) not in feat:
+            feat[(idx, l)] = recipe.features(idx, C, l)
+        return feat[(idx, l)]
+
+    inv0 = recipe.inv_depth_batch([recipe.depth_m(i) for i, _ in sel])
+    inv1 = recipe.inv_depth_batch([recipe.depth_m(j) for _, j in sel])
+    levels = []
+    for l in range(LEVELS):
+        k = 1 << l
+        dev = lambda a: torch.from_numpy(np.ascontiguousarray(a)).to(device)
+        levels.append(dict(
+            x0=dev(np.stack([fs(i, l)[0] for i, _ in sel])), x1=dev(np.stack([fs(j, l)[0] for _, j in sel])),
+            sigma0=dev(np.stack([fs(i, l)[1] for i, _ in sel])), sigma1=dev(np.stack([fs(j, l)[1] for _, j in sel])),
+            invD0=dev(recipe.max_pool(inv0, k)), invD1=dev(recipe.max_pool(inv1, k))))
+    K = torch.from_numpy(np.tile(recipe.K_FULL[None], (B, 1))).to(device)
+    return sel, levels, K
+
+
+def cpu_baseline(levels_gpu, K, R_gpu, t_gpu):
+    """Oracle (PyTorch-CPU restatement of the reference solver) on pair 0: 1 warm-up, best of 2."""
+    from oracle import ic_oracle as O
+    lv = [{k: v[:1].cpu() for k, v in d.items()} for d in levels_gpu]
+    lv = [dict(f0=d["x0"], f1=d["x1"], s0=d["sigma0"], s1=d["sigma1"], invD0=d["invD0"], invD1=d["invD1"]) for d in lv]
+    Kc = K[:1].cpu()
+    R0 = torch.eye(3)[None]
+    t0 = torch.zeros(1, 3, 1)
+    best = float("inf")
+    out = None
+    with torch.no_grad():
+        for rep in range(3):
+            t_start = time.perf_counter()
+            out = O.solve_pyramid(R0, t0, lv, Kc, iters=ITERS, remove_tru_sigma=True)
+            el = time.perf_counter() - t_start
+            if rep > 0:
+                best = min(best, el)
+    Ro, to = out
+    dR = (R_gpu[:1].cpu() - Ro).abs().max().item()
+    dt = (t_gpu[:1].cpu().view(1, 3) - to.view(1, 3)).abs().max().item()
+    # 3D end-point error between the two poses over frame-0 points (criterions.py:101-136)
+    from deep_prob_feature_track_amd.metrics import epe3d_between
+    d0 = 1.0 / lv[0]["invD0"].clamp(min=1e-6)
+    epe = epe3d_between(R_gpu[:1].cpu(), t_gpu[:1].cpu().view(1, 3), Ro, to.view(1, 3), d0,
+                        Kc, invalid=(lv[0]["invD0"] <= 0)).item()
+    return best, dR, dt, epe
+
+
+def main():
+    a = parse()
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        import torch.distributed as dist
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl")
+    device = torch.device("cuda", local)
+    torch.cuda.set_device(device)
+    from deep_prob_feature_track_amd import ic
+
+    B = a.batch_per_gpu
+    sel, levels, K = make_inputs(B, rank, device)
+    solver = ic.PyramidSolver(levels, K, iters=ITERS, remove_tru_sigma=True)
+    R_init = torch.eye(3, device=device).repeat(B, 1, 1).contiguous()
+    t_init = torch.zeros(B, 3, device=device)
+    R = R_init.clone()
+    t = t_init.clone()
+    gathered = torch.empty(world * B, 12, device=device) if world > 1 else None
+
+    def solve():
+        R.copy_(R_init)
+        t.copy_(t_init)
+        solver.run(R, t)
+
+    # eager warm-up (also validates), then capture the whole 4-level solve into one graph
+    solve()
+    torch.cuda.synchronize()
+    ic.check_status(solver.status)
+    graph = None
+    if not a.no_graph:
+        s = torch.cuda.Stream(device)
+        s.wait_stream(torch.cuda.current_stream(device))
+        with torch.cuda.stream(s):
+            solve()
+        torch.cuda.current_stream(device).wait_stream(s)
+        graph = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(graph):
+            solve()
+        torch.cuda.synchronize()
+
+    def step():
+        if graph is not None:
+            graph.replay()
+        else:
+            solve()
+        if world > 1:
+            import torch.distributed as dist
+            dist.all_gather_into_tensor(gathered, torch.cat((R.view(B, 9), t), 1))
+
+    def barrier():
+        if world > 1:
+            import torch.distributed as dist
+            dist.barrier()
+
+    for _ in range(a.warmup):
+        step()
+    torch.cuda.synchronize()
+    barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(a.steps):
+        step()
+    torch.cuda.synchronize()
+    barrier()
+    torch.cuda.synchronize()
+    elapsed = time.perf_counter() - t0
+    if world > 1:
+        import torch.distributed as dist
+        e = torch.tensor([elapsed], device=device, dtype=torch.float64)
+        dist.all_reduce(e, op=dist.ReduceOp.MAX)
+        elapsed = e.item()
+    ic.check_status(solver.status)
+    ms_per_step = elapsed / a.steps * 1e3
+    iters_total = world * B * LEVELS * ITERS * a.steps
+    value = iters_total / elapsed
+
+    # ---- roofline of the dominant kernel: the L0 fused reduce, timed with HIP events
+    # on the stream it is launched on (the current stream).
+    Rk, tk = R.clone(), t.clone()
+    for _ in range(3):
+        solver.reduce_only(0, Rk, tk)
+    ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    ev0.record()
+    for _ in range(a.kernel_reps):
+        solver.reduce_only(0, Rk, tk)
+    ev1.record()
+    torch.cuda.synchronize()
+    kern_us = ev0.elapsed_time(ev1) / a.kernel_reps * 1e3
+    alg_bytes = solver.algorithmic_bytes(0)
+    achieved = alg_bytes / (kern_us * 1e-6) / 1e9
+
+    cpu = None
+    if rank == 0 and world == 1 and not a.no_cpu_baseline:
+        best, dR, dt, epe = cpu_baseline(levels, K, R, t)
+        cpu = {"value": LEVELS * ITERS / best, "unit": "IC iterations/s",
+               "cores": torch.get_num_threads(), "kind": "port",
+               "sample": "1 pair, 640x480 C=32, 4 levels x 3 iters, oracle/ic_oracle.py (PyTorch-CPU fp32 "
+                         "restatement of algorithms.py:611-723), best of 2 after 1 warm-up",
+               "seconds_per_pair": best, "gpu_vs_oracle_max_abs_dR": dR, "gpu_vs_oracle_max_abs_dt": dt,
+               "gpu_vs_oracle_3dpe_m": epe}
+
+    if rank == 0:
+        line = {
+            "metric": "IC solver iters/sec (640x480, C=32, 4-level)",
+            "value": value, "unit": "IC iterations/s (all levels, 12 per pair)",
+            "n_gpus": world, "steps": a.steps, "warmup": a.warmup, "ms_per_step": ms_per_step,
+            "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "f32",
+            "data": "synthetic: deterministic triangle-wave features of the 5 TUM fr1/desk example frames",
+            "config": {"workload": "cfg2/cfg3 shard: 640x480, C=32, Cs=1, 4 levels x 3 GN iters, "
+                                   "remove_tru_sigma, B pairs per GPU", "pairs_per_gpu": B,
+                       "global_batch": world * B, "parallelism": f"pair-sharded x{world}, RCCL all-gather of poses",
+                       "graph": graph is not None},
+            "pairs_per_s": world * B * a.steps / elapsed,
+            "l0_iters_per_s": world * B * ITERS * a.steps / elapsed,
+            "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                         "frac": achieved / HBM_PEAK_GBS, "traffic": None,
+                         "kernel": "ic_reduce_kernel<32,true> (level 0)", "kernel_us": kern_us,
+                         "algorithmic_bytes_per_launch": alg_bytes},
+            "cpu_baseline": cpu,
+        }
+        print(json.dumps(line), flush=True)
+    if world > 1:
+        import torch.distributed as dist
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

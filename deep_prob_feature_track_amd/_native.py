@@ -1,0 +1,80 @@
+"""ctypes binding of libdpft_ic.so (C ABI: include/dpft_ic.h).
+
+The library is loaded only after torch, so its `libamdhip64.so.7` dependency
+resolves to the HIP runtime torch already mapped (one runtime, one set of
+streams).  There is no fallback: if the shared object is missing or fails to
+load, every call raises.
+"""
+import ctypes
+import os
+
+import torch  # noqa: F401  (must be imported before the HIP library, see above)
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "libdpft_ic.so")
+
+REMOVE_TRU_SIGMA = 0x1
+COMBINE_ICP = 0x2
+STATUS_NONFINITE = 0x1
+ABI_VERSION = 1
+
+
+class LevelDesc(ctypes.Structure):
+    _fields_ = [
+        ("B", ctypes.c_int32), ("C", ctypes.c_int32), ("Cs", ctypes.c_int32),
+        ("H", ctypes.c_int32), ("W", ctypes.c_int32), ("iters", ctypes.c_int32),
+        ("flags", ctypes.c_uint32), ("icp_weight", ctypes.c_float),
+    ]
+
+
+class LevelTensors(ctypes.Structure):
+    _fields_ = [
+        ("f0", ctypes.c_void_p), ("f1", ctypes.c_void_p), ("s0", ctypes.c_void_p), ("s1", ctypes.c_void_p),
+        ("invD0", ctypes.c_void_p), ("invD1", ctypes.c_void_p), ("depth0", ctypes.c_void_p),
+        ("depth1", ctypes.c_void_p), ("mask0", ctypes.c_void_p), ("mask1", ctypes.c_void_p),
+        ("K", ctypes.c_void_p), ("status", ctypes.c_void_p),
+    ]
+
+
+EXPORTS = ("dpft_workspace_size", "dpft_ic_solve_level", "dpft_ic_iterate", "dpft_ic_residual_level",
+           "dpft_ic_reduce_only", "dpft_ic_debug_pixels", "dpft_version", "dpft_last_error")
+
+_lib = None
+
+
+def lib():
+    """Load (once) and return the CDLL; raises if the native library is unavailable."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        raise RuntimeError(f"{LIB_PATH} is missing: build it with `python -c 'import __graft_entry__ as g; g.build()'`")
+    L = ctypes.CDLL(LIB_PATH, mode=ctypes.RTLD_GLOBAL)
+    P = ctypes.POINTER
+    vp, sz = ctypes.c_void_p, ctypes.c_size_t
+    L.dpft_workspace_size.argtypes = [P(LevelDesc)]
+    L.dpft_workspace_size.restype = sz
+    L.dpft_ic_solve_level.argtypes = [P(LevelDesc), P(LevelTensors), vp, vp, vp, vp, vp, sz, vp]
+    L.dpft_ic_solve_level.restype = ctypes.c_int
+    L.dpft_ic_iterate.argtypes = [P(LevelDesc), P(LevelTensors), vp, vp, vp, vp, vp, ctypes.c_int, vp, sz, vp]
+    L.dpft_ic_iterate.restype = ctypes.c_int
+    L.dpft_ic_residual_level.argtypes = [P(LevelDesc), P(LevelTensors), vp, vp, vp, vp, sz, vp]
+    L.dpft_ic_residual_level.restype = ctypes.c_int
+    L.dpft_ic_reduce_only.argtypes = [P(LevelDesc), P(LevelTensors), vp, vp, vp, sz, vp]
+    L.dpft_ic_reduce_only.restype = ctypes.c_int
+    L.dpft_ic_debug_pixels.argtypes = [P(LevelDesc), P(LevelTensors), vp, vp, vp, vp, sz, vp]
+    L.dpft_ic_debug_pixels.restype = ctypes.c_int
+    L.dpft_version.argtypes = []
+    L.dpft_version.restype = ctypes.c_int
+    L.dpft_last_error.argtypes = []
+    L.dpft_last_error.restype = ctypes.c_char_p
+    if L.dpft_version() != ABI_VERSION:
+        raise RuntimeError(f"libdpft_ic ABI {L.dpft_version()} != expected {ABI_VERSION}")
+    _lib = L
+    return L
+
+
+def check(rc, what):
+    if rc != 0:
+        msg = lib().dpft_last_error().decode(errors="replace")
+        raise RuntimeError(f"{what} failed ({rc}): {msg}")

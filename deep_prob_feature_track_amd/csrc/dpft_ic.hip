@@ -1,0 +1,1218 @@
+// libdpft_ic.so -- gfx950 (MI355X) kernels + C ABI for the trust-region
+// inverse-compositional (U_IC) solver of Deep Probabilistic Feature-metric
+// Tracking.  ABI and semantics: include/dpft_ic.h.
+//
+// One Gauss-Newton iteration at one pyramid level is two launches:
+//
+//   ic_reduce_kernel   fused, HBM-bound pass over every pixel of every pair:
+//                      inverse-depth warp (geometry.py:291-323), bilinear
+//                      gathers of invD1 / f1 / sigma1 (geometry.py:353-365),
+//                      occlusion + object masks (geometry.py:334-350,
+//                      algorithms.py:1999-2008), uncertainty-weighted residual
+//                      (algorithms.py:1960-1989), Sobel gradients of f0 and
+//                      sigma0 recomputed from an LDS tile (algorithms.py:
+//                      1844-1865, never stored), the per-channel inverse
+//                      Jacobian (algorithms.py:867-887, 1867-1917) folded into
+//                      channel sums, and the 21 + 6 normal-equation partials
+//                      (algorithms.py:812-834).  Each workgroup writes one
+//                      fixed-size record: no atomics, deterministic.
+//   ic_finalize_kernel one workgroup per pair: fixed-order fp64 reduction of
+//                      that pair's records, the batch-global truncated-sigma
+//                      correction, Levenberg damping, fp64 6x6 solve and the
+//                      SE(3) update (algorithms.py:2017-2103), in place.
+//
+// J is never materialised: per pixel and channel the reference's J_c is
+// -(a_c Jx + b_c Jy), so sum_c J_c J_c^T = Saa JxJx^T + Sab (JxJy^T + JyJx^T)
+// + Sbb JyJy^T and sum_c J_c rw_c = -(Sar Jx + Sbr Jy): channel sums per pixel
+// replace the [B,C,HW,6] tensor of algorithms.py:878-885.
+//
+// Truncated sigma (algorithms.py:1975-1980) compares sigma_r against its min /
+// max over the WHOLE batch, which is only known after the pass.  Because J is
+// unmasked the flag only changes JtR, so each record also carries the block's
+// sigma_r extrema and the JtR correction sum_c J_c (1e-6 - rw_c) of the
+// not-yet-invalid pixels that attain them; the finalize applies the
+// corrections of the blocks whose extremum equals the global one.
+//
+// The equality tests of that mask (and u > 0 of the in-view test) make the
+// result depend on the last bit of the warped coordinates, so the warp and the
+// sampler reproduce the reference's CPU arithmetic op for op (measured, see
+// warp_point / bil4); everywhere else the compiler may contract freely.
+
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cmath>
+#include <cstdarg>
+#include <cstdint>
+#include <cstdio>
+#include <cstring>
+
+#include "dpft_ic.h"
+
+namespace {
+
+constexpr int kThreads = 256;          // 4 waves of 64
+constexpr int kTileW = 64;             // one wave = 64 consecutive pixels of a row
+constexpr int kRowsPerStep = 4;        // one row per wave per step
+constexpr int kCK = 8;                 // channels staged in LDS per unit
+constexpr int kLdsW = kTileW + 2;      // 1-pixel halo each side
+constexpr int kLdsH = kRowsPerStep + 2;
+constexpr int kMaxSteps = 4;           // up to 16 rows per workgroup
+
+// ---- reduce-record layout (floats) ------------------------------------------
+constexpr int kRec = 48;
+constexpr int R_NINV = 27;    // invalid pixels (occlusion | masks | sigma0-trunc)
+constexpr int R_MN_ALL = 28;  // min of sigma_r over every channel
+constexpr int R_MN0 = 29;     // min of sigma_r channel 0
+constexpr int R_CMN = 30;     // 6: JtR correction of the pixels at R_MN0
+constexpr int R_NMN = 36;     // count of those pixels
+constexpr int R_MX_ALL = 37;
+constexpr int R_MX0 = 38;
+constexpr int R_CMX = 39;     // 6
+constexpr int R_NMX = 45;
+
+// ---- residual-record layout --------------------------------------------------
+constexpr int L_SUM = 0, L_NINV = 1, L_MN_ALL = 2, L_MN0 = 3, L_LMN = 4, L_NMN = 5,
+              L_MX_ALL = 6, L_MX0 = 7, L_LMX = 8, L_NMX = 9;
+
+// workspace: [ctrl 256 B][records]
+constexpr size_t kCtrlBytes = 256;
+
+thread_local char g_err[512] = "";
+
+int fail(int code, const char* fmt, ...) {
+  va_list ap;
+  va_start(ap, fmt);
+  vsnprintf(g_err, sizeof(g_err), fmt, ap);
+  va_end(ap);
+  return code;
+}
+
+// ------------------------------------------------------------------ device utils
+__device__ __forceinline__ uint32_t enc_ord(float f) {
+  uint32_t u = __float_as_uint(f);
+  return (u & 0x80000000u) ? ~u : (u | 0x80000000u);
+}
+__device__ __forceinline__ float dec_ord(uint32_t e) {
+  uint32_t u = (e & 0x80000000u) ? (e & 0x7fffffffu) : ~e;
+  return __uint_as_float(u);
+}
+
+__device__ __forceinline__ int wave_id() { return __builtin_amdgcn_readfirstlane(threadIdx.x >> 6); }
+
+// XCD-aware bijective remap: the dispatcher deals workgroups round-robin over the
+// 8 XCDs, so give the workgroups that share an XCD consecutive tiles (vertically
+// adjacent tiles share halo rows through that XCD's L2).  Speed only.
+__device__ __forceinline__ int xcd_remap(int orig, int n) {
+  const int xcd = orig & 7, q = n >> 3, r = n & 7;
+  const int base = xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q;
+  return base + (orig >> 3);
+}
+
+struct Taps {
+  int o00, o01, o10, o11;
+  float nw, ne, sw, se;
+};
+
+// geometry.py:359-364 normalises u,v to [-1,1]; grid_sample(align_corners=True,
+// padding_mode='border') maps back with (g + 1) * (size - 1) / 2, clamps to
+// [0, size-1], and weighs the four neighbours by products of the distances.
+__device__ __forceinline__ Taps make_taps(float u, float v, int H, int W) {
+#pragma clang fp contract(off)
+  const float sx = (float)(W - 1) * 0.5f;
+  const float sy = (float)(H - 1) * 0.5f;
+  float ix = ((u / sx) - 1.0f + 1.0f) * sx;
+  float iy = ((v / sy) - 1.0f + 1.0f) * sy;
+  ix = fminf(fmaxf(ix, 0.0f), (float)(W - 1));
+  iy = fminf(fmaxf(iy, 0.0f), (float)(H - 1));
+  const float fx0 = floorf(ix), fy0 = floorf(iy);
+  const int x0 = (int)fx0, y0 = (int)fy0;
+  const float w = ix - fx0, e = 1.0f - w;
+  const float n = iy - fy0, s = 1.0f - n;
+  const int x1 = min(x0 + 1, W - 1), y1 = min(y0 + 1, H - 1);
+  Taps t;
+  t.o00 = y0 * W + x0;
+  t.o01 = y0 * W + x1;
+  t.o10 = y1 * W + x0;
+  t.o11 = y1 * W + x1;
+  t.nw = s * e;
+  t.ne = s * w;
+  t.sw = n * e;
+  t.se = n * w;
+  return t;
+}
+
+// An out-of-range neighbour always has weight exactly 0 under border clamping,
+// so reading the clamped pixel instead of a masked zero changes nothing.  The
+// accumulation is the fused chain the CPU grid sampler compiles to,
+// fma(d, se, fma(c, sw, fma(b, ne, a * nw))): measured bit-identical to
+// torch.nn.functional.grid_sample on 2e5 random samples.
+__device__ __forceinline__ float bil4(float a, float b, float c, float d, const Taps& t) {
+#pragma clang fp contract(off)
+  return __builtin_fmaf(d, t.se, __builtin_fmaf(c, t.sw, __builtin_fmaf(b, t.ne, a * t.nw)));
+}
+__device__ __forceinline__ float bil(const float* __restrict__ p, const Taps& t) {
+  return bil4(p[t.o00], p[t.o01], p[t.o10], p[t.o11], t);
+}
+__device__ __forceinline__ float bil_u8(const uint8_t* __restrict__ p, const Taps& t) {
+  return bil4((float)p[t.o00], (float)p[t.o01], (float)p[t.o10], (float)p[t.o11], t);
+}
+
+struct Warp {
+  float u, v, iz, xr, yr;
+};
+
+// Inverse-depth warp of pixel (x, y), op for op as the reference evaluates it on
+// the CPU (geometry.py:63-85, 291-323): px = (u - cx) / fx; torch.bmm(R, [px,py,1])
+// = fma(R1, py, R0 * px) + R2 per row (measured bit-identical for every
+// shape used); + t * invD; u = (X / Z) * fx + cx; iz = invD / Z.
+__device__ __forceinline__ Warp warp_point(int x, int y, float d, const float* __restrict__ Rm,
+                                           const float* __restrict__ tv, float fx, float fy, float cx, float cy) {
+#pragma clang fp contract(off)
+  Warp w;
+  w.xr = ((float)x - cx) / fx;
+  w.yr = ((float)y - cy) / fy;
+  const float X = (__builtin_fmaf(Rm[1], w.yr, Rm[0] * w.xr) + Rm[2]) + tv[0] * d;
+  const float Y = (__builtin_fmaf(Rm[4], w.yr, Rm[3] * w.xr) + Rm[5]) + tv[1] * d;
+  const float Z = (__builtin_fmaf(Rm[7], w.yr, Rm[6] * w.xr) + Rm[8]) + tv[2] * d;
+  w.u = (X / Z) * fx + cx;
+  w.v = (Y / Z) * fy + cy;
+  w.iz = d / Z;
+  return w;
+}
+
+struct IterParams {
+  const float* f0;
+  const float* f1;
+  const float* s0;
+  const float* s1;
+  const float* invD0;
+  const float* invD1;
+  const uint8_t* mask0;
+  const uint8_t* mask1;
+  const float* K;
+  const float* R;
+  const float* t;
+  int B, C, Cs, H, W;
+  int tiles_x, tiles_y, steps, nblocks;
+  uint32_t flags;
+  const uint32_t* ctrl;  // [0]=enc min sigma0, [1]=enc max sigma0
+  float* rec;
+};
+
+// Per-pixel state that lives across the channel loop of one step.
+struct PixelFrame {
+  Taps tp;
+  float d, xr, yr;
+  float inv_s, kk, hx, hy, sr0, srmin, srmax;
+  bool invalid;
+};
+
+// Warp, taps, occlusion (geometry.py:334-350) and object masks (algorithms.py:1999-2008).
+__device__ __forceinline__ void setup_pixel(const IterParams& p, int b, int x, int y, float d,
+                                            const float* __restrict__ Rm, const float* __restrict__ tv, float fx,
+                                            float fy, float cx, float cy, PixelFrame& px) {
+  const int W = p.W, H = p.H, HW = H * W;
+  const Warp w = warp_point(x, y, d, Rm, tv, fx, fy, cx, cy);
+  px.tp = make_taps(w.u, w.v, H, W);
+  px.d = d;
+  px.xr = w.xr;
+  px.yr = w.yr;
+  const float d1w = bil(p.invD1 + (size_t)b * HW, px.tp);
+  const bool ok = (w.iz > d1w - 0.1f) && (w.u > 0.0f) && (w.u < (float)W) && (w.v > 0.0f) && (w.v < (float)H);
+  bool inv = !ok;
+  if (p.mask0) inv = inv || (p.mask0[(size_t)b * HW + y * W + x] == 0);
+  if (p.mask1) inv = inv || !(bil_u8(p.mask1 + (size_t)b * HW, px.tp) > 0.0f);
+  px.invalid = inv;
+}
+
+// Unit-normalised 3x3 Sobel of an LDS tile around (row r, col c)
+// (algorithms.py:1852-1863: cross-correlation with [-1 0 1; -2 0 2; -1 0 1]).
+__device__ __forceinline__ void sobel_lds(const float* __restrict__ L, int r, int c, float& gx, float& gy,
+                                          float& ctr) {
+  const float* a = L + (r - 1) * kLdsW + c;
+  const float* m = L + r * kLdsW + c;
+  const float* z = L + (r + 1) * kLdsW + c;
+  const float v00 = a[-1], v01 = a[0], v02 = a[1];
+  const float v10 = m[-1], v11 = m[0], v12 = m[1];
+  const float v20 = z[-1], v21 = z[0], v22 = z[1];
+  const float x = (v02 - v00) + 2.0f * (v12 - v10) + (v22 - v20);
+  const float y = (v20 + 2.0f * v21 + v22) - (v00 + 2.0f * v01 + v02);
+  const float inv = rsqrtf(x * x + y * y + 1e-8f);
+  gx = x * inv;
+  gy = y * inv;
+  ctr = v11;
+}
+
+// Warp Jacobian at the origin, xi = [rot, trs] (algorithms.py:1908-1917).
+__device__ __forceinline__ void warp_jac(float xr, float yr, float d, float fx, float fy, float* Jx, float* Jy) {
+  const float xy = xr * yr;
+  Jx[0] = -xy * fx;
+  Jx[1] = (1.0f + xr * xr) * fx;
+  Jx[2] = -yr * fx;
+  Jx[3] = d * fx;
+  Jx[4] = 0.0f;
+  Jx[5] = -d * xr * fx;
+  Jy[0] = (-1.0f - yr * yr) * fy;
+  Jy[1] = xy * fy;
+  Jy[2] = xr * fy;
+  Jy[3] = 0.0f;
+  Jy[4] = d * fy;
+  Jy[5] = -d * yr * fy;
+}
+
+struct Extremum {
+  float all;   // extremum over every channel (decides the global value)
+  float v0;    // extremum of channel 0 (decides which pixels are flagged)
+  float c[6];  // JtR correction of the not-yet-invalid pixels at v0
+  float n;     // their count
+};
+
+template <bool IS_MIN>
+__device__ __forceinline__ void ext_merge(Extremum& e, float all, float v0, const float* c, float n) {
+  e.all = IS_MIN ? fminf(e.all, all) : fmaxf(e.all, all);
+  const bool better = IS_MIN ? (v0 < e.v0) : (v0 > e.v0);
+  if (better) {
+    e.v0 = v0;
+#pragma unroll
+    for (int k = 0; k < 6; ++k) e.c[k] = c[k];
+    e.n = n;
+  } else if (v0 == e.v0) {
+#pragma unroll
+    for (int k = 0; k < 6; ++k) e.c[k] += c[k];
+    e.n += n;
+  }
+}
+
+template <bool IS_MIN>
+__device__ __forceinline__ void ext_wave_reduce(Extremum& e) {
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) {
+    Extremum o;
+    o.all = __shfl_xor(e.all, off);
+    o.v0 = __shfl_xor(e.v0, off);
+#pragma unroll
+    for (int k = 0; k < 6; ++k) o.c[k] = __shfl_xor(e.c[k], off);
+    o.n = __shfl_xor(e.n, off);
+    ext_merge<IS_MIN>(e, o.all, o.v0, o.c, o.n);
+  }
+}
+
+// ---------------------------------------------------------------- LDS staging
+// A stage unit = one step (4 image rows + 1 halo row above and below) x one
+// chunk of <= kCK channels of f0, plus sigma0 (its single plane at chunk 0 when
+// Cs == 1, the chunk's planes otherwise).  The unit is a list of "rows": row q
+// is plane-row (q % 6) of the q/6-th staged plane.  Wave w loads rows w, w+4,
+// ...: one 64-lane load per row (LDS cols 0..63 = image cols x0-1 .. x0+62,
+// clamped = replicate padding) plus ONE load per wave for all its rows' right
+// halo (cols 64, 65).  Addresses are a scalar row base plus a fixed per-lane
+// column, so the loads cost no vector ALU; they are issued one unit ahead into
+// registers and written to the other LDS buffer after the current unit's math.
+template <bool CS1>
+struct StageCfg {
+  static constexpr int kPlanes = CS1 ? kCK + 1 : 2 * kCK;  // max planes per unit
+  static constexpr int kRows = kPlanes * kLdsH;            // max rows per unit
+  static constexpr int kRowsPerWave = (kRows + 3) / 4;
+  static constexpr int kBufFloats = kRows * kLdsW;
+};
+
+struct UnitGeom {
+  int c0, nc, nplanes, y0;  // nplanes = f0 planes + sigma0 planes staged in this unit
+};
+
+// plane p of a unit -> source pointer
+template <bool CS1>
+__device__ __forceinline__ const float* plane_src(const float* f0b, const float* s0b, int HW, const UnitGeom& g,
+                                                  int pidx) {
+  if (pidx < g.nc) return f0b + (size_t)(g.c0 + pidx) * HW;
+  const int sp = pidx - g.nc;
+  return s0b + (size_t)(CS1 ? 0 : g.c0 + sp) * HW;
+}
+
+template <bool CS1>
+__device__ __forceinline__ void stage_load(float (&reg)[StageCfg<CS1>::kRowsPerWave], float& halo,
+                                           const float* f0b, const float* s0b, const UnitGeom& g, int H, int W,
+                                           int x0, int wave, int lane) {
+  const int HW = H * W;
+  const int nrows = g.nplanes * kLdsH;
+  const int col = min(max(x0 - 1 + lane, 0), W - 1);
+#pragma unroll
+  for (int j = 0; j < StageCfg<CS1>::kRowsPerWave; ++j) {
+    const int q = wave + 4 * j;  // wave-uniform
+    if (q < nrows) {
+      const int pl = q / kLdsH, r = q - pl * kLdsH;
+      const int gy = min(max(g.y0 - 1 + r, 0), H - 1);
+      reg[j] = plane_src<CS1>(f0b, s0b, HW, g, pl)[gy * W + col];
+    }
+  }
+  // right halo of every row of this wave: lane l -> row j = l >> 1, col 64 + (l & 1)
+  const int j = lane >> 1;
+  const int q = wave + 4 * j;
+  if (j < StageCfg<CS1>::kRowsPerWave && q < nrows) {
+    const int pl = q / kLdsH, r = q - pl * kLdsH;
+    const int gy = min(max(g.y0 - 1 + r, 0), H - 1);
+    const int hc = min(x0 + 63 + (lane & 1), W - 1);
+    halo = plane_src<CS1>(f0b, s0b, HW, g, pl)[gy * W + hc];
+  }
+}
+
+template <bool CS1>
+__device__ __forceinline__ void stage_store(float* __restrict__ buf, const float (&reg)[StageCfg<CS1>::kRowsPerWave],
+                                            float halo, const UnitGeom& g, int wave, int lane) {
+  const int nrows = g.nplanes * kLdsH;
+#pragma unroll
+  for (int j = 0; j < StageCfg<CS1>::kRowsPerWave; ++j) {
+    const int q = wave + 4 * j;
+    if (q < nrows) buf[q * kLdsW + lane] = reg[j];
+  }
+  const int j = lane >> 1;
+  const int q = wave + 4 * j;
+  if (j < StageCfg<CS1>::kRowsPerWave && q < nrows) buf[q * kLdsW + 64 + (lane & 1)] = halo;
+}
+
+// ============================================================ fused reduce kernel
+template <int CT, bool CS1, bool TRU>
+__global__ __launch_bounds__(kThreads) void ic_reduce_kernel(IterParams p) {
+  using SC = StageCfg<CS1>;
+  const int C = CT > 0 ? CT : p.C;
+  __shared__ float lds_buf[2][SC::kBufFloats];
+  __shared__ float lds_ext[TRU ? 2 * 7 : 1][kThreads];  // extremum corrections (6 + count), min then max
+  __shared__ float red[4][kRec];
+
+  const int tid = threadIdx.x, lane = tid & 63, wave = wave_id();
+  const int bid = xcd_remap(blockIdx.x, p.nblocks);
+  const int tx = bid % p.tiles_x;
+  const int rest = bid / p.tiles_x;
+  const int ty = rest % p.tiles_y;
+  const int b = rest / p.tiles_y;
+  const int W = p.W, H = p.H, HW = H * W;
+
+  const float fx = p.K[4 * b + 0], fy = p.K[4 * b + 1], cx = p.K[4 * b + 2], cy = p.K[4 * b + 3];
+  float Rm[9], tv[3];
+#pragma unroll
+  for (int k = 0; k < 9; ++k) Rm[k] = p.R[9 * b + k];
+#pragma unroll
+  for (int k = 0; k < 3; ++k) tv[k] = p.t[3 * b + k];
+  const float g0min = TRU ? dec_ord(p.ctrl[0]) : 0.f, g0max = TRU ? dec_ord(p.ctrl[1]) : 0.f;
+
+  const float* f0b = p.f0 + (size_t)b * C * HW;
+  const float* f1b = p.f1 + (size_t)b * C * HW;
+  const float* s0b = p.s0 + (size_t)b * p.Cs * HW;
+  const float* s1b = p.s1 + (size_t)b * p.Cs * HW;
+  const float* d0b = p.invD0 + (size_t)b * HW;
+
+  float acc[27];
+#pragma unroll
+  for (int k = 0; k < 27; ++k) acc[k] = 0.0f;
+  float ninv = 0.0f;
+  float mn_all = INFINITY, mn0 = INFINITY, mx_all = -INFINITY, mx0 = -INFINITY;
+  if (TRU) {
+#pragma unroll
+    for (int k = 0; k < 14; ++k) lds_ext[k][tid] = 0.0f;
+  }
+
+  const int x0 = tx * kTileW;
+  const int x = x0 + lane;
+  const int nch = (C + kCK - 1) / kCK;
+  int nsteps = p.steps;
+  {
+    const int last_row = (ty * p.steps + nsteps) * kRowsPerStep;  // steps fully below the image: skip
+    const int over = last_row - H;
+    if (over >= kRowsPerStep) nsteps -= over / kRowsPerStep;
+  }
+  auto unit_geom = [&](int s, int k) {
+    UnitGeom g;
+    g.c0 = k * kCK;
+    g.nc = min(kCK, C - g.c0);
+    g.nplanes = g.nc + (CS1 ? (k == 0 ? 1 : 0) : g.nc);
+    g.y0 = (ty * p.steps + s) * kRowsPerStep;
+    return g;
+  };
+
+  float reg[SC::kRowsPerWave];
+  float halo = 0.0f;
+  {
+    const UnitGeom g0 = unit_geom(0, 0);
+    stage_load<CS1>(reg, halo, f0b, s0b, g0, H, W, x0, wave, lane);
+    stage_store<CS1>(lds_buf[0], reg, halo, g0, wave, lane);
+  }
+  float d_next = 0.0f;
+  {
+    const int y = (ty * p.steps) * kRowsPerStep + wave;
+    if (x < W && y < H) d_next = d0b[y * W + x];
+  }
+  __syncthreads();
+
+  int u = 0;
+  for (int s = 0; s < nsteps; ++s) {
+    const int y = (ty * p.steps + s) * kRowsPerStep + wave;
+    const bool active = (x < W) && (y < H);
+    PixelFrame px;
+    px.invalid = true;
+    const float d = d_next;
+    if (active) setup_pixel(p, b, x, y, d, Rm, tv, fx, fy, cx, cy, px);
+    if (s + 1 < nsteps) {
+      const int yn = y + kRowsPerStep;
+      if (x < W && yn < H) d_next = d0b[yn * W + x];
+    }
+    float Saa = 0.f, Sab = 0.f, Sbb = 0.f, Sa = 0.f, Sb = 0.f, Sar = 0.f, Sbr = 0.f;
+
+    for (int k = 0; k < nch; ++k, ++u) {
+      const UnitGeom g = unit_geom(s, k);
+      // issue the next unit's loads first: they fly while this unit computes
+      const bool has_next = (k + 1 < nch) || (s + 1 < nsteps);
+      UnitGeom gn = g;
+      if (has_next) {
+        gn = (k + 1 < nch) ? unit_geom(s, k + 1) : unit_geom(s + 1, 0);
+        stage_load<CS1>(reg, halo, f0b, s0b, gn, H, W, x0, wave, lane);
+      }
+      const float* buf = lds_buf[u & 1];
+      const float* sbuf = buf + g.nc * kLdsH * kLdsW;  // sigma0 planes follow the f0 planes
+      if (active) {
+        if (CS1 && k == 0) {
+          float ctr;
+          sobel_lds(sbuf, wave + 1, lane + 1, px.hx, px.hy, ctr);
+          px.sr0 = bil(s1b, px.tp);
+          px.srmin = px.srmax = px.sr0;
+          const float sg = sqrtf(px.sr0 * px.sr0 + ctr * ctr);
+          px.inv_s = 1.0f / sg;
+          px.kk = ctr * (px.inv_s * px.inv_s * px.inv_s);
+          if (TRU) px.invalid = px.invalid || (ctr == g0min) || (ctr == g0max);
+        }
+#pragma unroll
+        for (int cc = 0; cc < kCK; ++cc) {
+          if (CT == 0 && cc >= g.nc) break;
+          if (CT > 0 && (CT % kCK) != 0 && cc >= g.nc) break;
+          const int c = g.c0 + cc;
+          float gx, gy, f0v;
+          sobel_lds(buf + cc * kLdsH * kLdsW, wave + 1, lane + 1, gx, gy, f0v);
+          float inv_s, kk, hx, hy;
+          if (CS1) {
+            inv_s = px.inv_s;
+            kk = px.kk;
+            hx = px.hx;
+            hy = px.hy;
+          } else {
+            float s0c;
+            sobel_lds(sbuf + cc * kLdsH * kLdsW, wave + 1, lane + 1, hx, hy, s0c);
+            const float src = bil(s1b + (size_t)c * HW, px.tp);
+            const float sg = sqrtf(src * src + s0c * s0c);
+            inv_s = 1.0f / sg;
+            kk = s0c * (inv_s * inv_s * inv_s);
+            if (c == 0) {
+              px.sr0 = src;
+              px.srmin = px.srmax = src;
+              if (TRU) px.invalid = px.invalid || (s0c == g0min) || (s0c == g0max);
+            } else {
+              px.srmin = fminf(px.srmin, src);
+              px.srmax = fmaxf(px.srmax, src);
+            }
+          }
+          const float fr = bil(f1b + (size_t)c * HW, px.tp);
+          const float r = fr - f0v;
+          const float rw = r * inv_s;
+          const float rk = r * kk;
+          const float a = -(gx * inv_s + rk * hx);
+          const float bq = -(gy * inv_s + rk * hy);
+          Saa += a * a;
+          Sab += a * bq;
+          Sbb += bq * bq;
+          Sa += a;
+          Sb += bq;
+          Sar += a * rw;
+          Sbr += bq * rw;
+        }
+      }
+      if (has_next) stage_store<CS1>(lds_buf[(u + 1) & 1], reg, halo, gn, wave, lane);
+      __syncthreads();
+    }
+    if (!active) continue;
+
+    float Jx[6], Jy[6];
+    warp_jac(px.xr, px.yr, px.d, fx, fy, Jx, Jy);
+    // weighted residual of invalid pixels is 1e-6 on every channel (algorithms.py:1982-1983)
+    const float cA = px.invalid ? 1e-6f * Sa : Sar;
+    const float cB = px.invalid ? 1e-6f * Sb : Sbr;
+    float P[6], Q[6];
+#pragma unroll
+    for (int i = 0; i < 6; ++i) {
+      P[i] = Saa * Jx[i] + Sab * Jy[i];
+      Q[i] = Sab * Jx[i] + Sbb * Jy[i];
+    }
+    int kq = 0;
+#pragma unroll
+    for (int i = 0; i < 6; ++i) {
+#pragma unroll
+      for (int j = i; j < 6; ++j) {
+        acc[kq] += P[i] * Jx[j] + Q[i] * Jy[j];
+        ++kq;
+      }
+    }
+#pragma unroll
+    for (int i = 0; i < 6; ++i) acc[21 + i] -= cA * Jx[i] + cB * Jy[i];
+    ninv += px.invalid ? 1.0f : 0.0f;
+
+    if (TRU) {
+      mn_all = fminf(mn_all, px.srmin);
+      mx_all = fmaxf(mx_all, px.srmax);
+      const bool le = px.sr0 <= mn0, ge = px.sr0 >= mx0;
+      if (le || ge) {
+        float corr[7];
+        const float dA = px.invalid ? 0.0f : (1e-6f * Sa - Sar);
+        const float dB = px.invalid ? 0.0f : (1e-6f * Sb - Sbr);
+#pragma unroll
+        for (int i = 0; i < 6; ++i) corr[i] = -(dA * Jx[i] + dB * Jy[i]);
+        corr[6] = px.invalid ? 0.0f : 1.0f;
+        if (le) {
+          const bool reset = px.sr0 < mn0;
+          mn0 = px.sr0;
+#pragma unroll
+          for (int i = 0; i < 7; ++i) lds_ext[i][tid] = (reset ? 0.0f : lds_ext[i][tid]) + corr[i];
+        }
+        if (ge) {
+          const bool reset = px.sr0 > mx0;
+          mx0 = px.sr0;
+#pragma unroll
+          for (int i = 0; i < 7; ++i) lds_ext[7 + i][tid] = (reset ? 0.0f : lds_ext[7 + i][tid]) + corr[i];
+        }
+      }
+    }
+  }
+
+  // ---- workgroup reduction -> one record (fixed order: deterministic)
+#pragma unroll
+  for (int k = 0; k < 27; ++k) {
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) acc[k] += __shfl_xor(acc[k], off);
+  }
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) ninv += __shfl_xor(ninv, off);
+  Extremum emn, emx;
+  if (TRU) {
+    emn.all = mn_all;
+    emn.v0 = mn0;
+    emx.all = mx_all;
+    emx.v0 = mx0;
+#pragma unroll
+    for (int k = 0; k < 6; ++k) {
+      emn.c[k] = lds_ext[k][tid];
+      emx.c[k] = lds_ext[7 + k][tid];
+    }
+    emn.n = lds_ext[6][tid];
+    emx.n = lds_ext[13][tid];
+    ext_wave_reduce<true>(emn);
+    ext_wave_reduce<false>(emx);
+  }
+  if (lane == 0) {
+#pragma unroll
+    for (int k = 0; k < 27; ++k) red[wave][k] = acc[k];
+    red[wave][R_NINV] = ninv;
+    if (TRU) {
+      red[wave][R_MN_ALL] = emn.all;
+      red[wave][R_MN0] = emn.v0;
+      red[wave][R_NMN] = emn.n;
+      red[wave][R_MX_ALL] = emx.all;
+      red[wave][R_MX0] = emx.v0;
+      red[wave][R_NMX] = emx.n;
+#pragma unroll
+      for (int k = 0; k < 6; ++k) {
+        red[wave][R_CMN + k] = emn.c[k];
+        red[wave][R_CMX + k] = emx.c[k];
+      }
+    }
+  }
+  __syncthreads();
+  float* out = p.rec + (size_t)bid * kRec;
+  if (tid < 28) {
+    out[tid] = ((red[0][tid] + red[1][tid]) + red[2][tid]) + red[3][tid];
+  } else if (TRU && tid == 64) {
+    Extremum e;
+    e.all = red[0][R_MN_ALL];
+    e.v0 = red[0][R_MN0];
+    e.n = red[0][R_NMN];
+    for (int k = 0; k < 6; ++k) e.c[k] = red[0][R_CMN + k];
+    for (int w = 1; w < 4; ++w) ext_merge<true>(e, red[w][R_MN_ALL], red[w][R_MN0], &red[w][R_CMN], red[w][R_NMN]);
+    out[R_MN_ALL] = e.all;
+    out[R_MN0] = e.v0;
+    out[R_NMN] = e.n;
+    for (int k = 0; k < 6; ++k) out[R_CMN + k] = e.c[k];
+  } else if (TRU && tid == 128) {
+    Extremum e;
+    e.all = red[0][R_MX_ALL];
+    e.v0 = red[0][R_MX0];
+    e.n = red[0][R_NMX];
+    for (int k = 0; k < 6; ++k) e.c[k] = red[0][R_CMX + k];
+    for (int w = 1; w < 4; ++w) ext_merge<false>(e, red[w][R_MX_ALL], red[w][R_MX0], &red[w][R_CMX], red[w][R_NMX]);
+    out[R_MX_ALL] = e.all;
+    out[R_MX0] = e.v0;
+    out[R_NMX] = e.n;
+    for (int k = 0; k < 6; ++k) out[R_CMX + k] = e.c[k];
+  }
+}
+
+// ============================================================ residual-only kernel
+template <bool CS1>
+__global__ __launch_bounds__(kThreads) void ic_residual_kernel(IterParams p) {
+  __shared__ float red[4][16];
+  const int tid = threadIdx.x, lane = tid & 63, wave = wave_id();
+  const int bid = xcd_remap(blockIdx.x, p.nblocks);
+  const int tx = bid % p.tiles_x;
+  const int rest = bid / p.tiles_x;
+  const int ty = rest % p.tiles_y;
+  const int b = rest / p.tiles_y;
+  const int W = p.W, H = p.H, HW = H * W, C = p.C;
+  const bool tru = (p.flags & DPFT_REMOVE_TRU_SIGMA) != 0;
+  const float fx = p.K[4 * b + 0], fy = p.K[4 * b + 1], cx = p.K[4 * b + 2], cy = p.K[4 * b + 3];
+  float Rm[9], tv[3];
+  for (int k = 0; k < 9; ++k) Rm[k] = p.R[9 * b + k];
+  for (int k = 0; k < 3; ++k) tv[k] = p.t[3 * b + k];
+  const float g0min = dec_ord(p.ctrl[0]), g0max = dec_ord(p.ctrl[1]);
+  const float* f0b = p.f0 + (size_t)b * C * HW;
+  const float* f1b = p.f1 + (size_t)b * C * HW;
+  const float* s0b = p.s0 + (size_t)b * p.Cs * HW;
+  const float* s1b = p.s1 + (size_t)b * p.Cs * HW;
+
+  float sum = 0.f, ninv = 0.f;
+  float mn_all = INFINITY, mn0 = INFINITY, lmn = 0.f, nmn = 0.f;
+  float mx_all = -INFINITY, mx0 = -INFINITY, lmx = 0.f, nmx = 0.f;
+  for (int step = 0; step < p.steps; ++step) {
+    const int y = (ty * p.steps + step) * kRowsPerStep + wave, x = tx * kTileW + lane;
+    if (x >= W || y >= H) continue;
+    const int pix = y * W + x;
+    PixelFrame px;
+    setup_pixel(p, b, x, y, p.invD0[(size_t)b * HW + pix], Rm, tv, fx, fy, cx, cy, px);
+    float srr = 0.f, smin = INFINITY, smax = -INFINITY, sr0 = 0.f, s00 = 0.f;
+    for (int c = 0; c < C; ++c) {
+      const int cs = CS1 ? 0 : c;
+      const float s0c = s0b[(size_t)cs * HW + pix];
+      const float src = bil(s1b + (size_t)cs * HW, px.tp);
+      if (c == 0) {
+        sr0 = src;
+        s00 = s0c;
+      }
+      smin = fminf(smin, src);
+      smax = fmaxf(smax, src);
+      const float r = bil(f1b + (size_t)c * HW, px.tp) - f0b[(size_t)c * HW + pix];
+      const float rw = r / sqrtf(src * src + s0c * s0c);
+      srr += rw * rw;
+    }
+    bool inv = px.invalid;
+    if (tru) inv = inv || (s00 == g0min) || (s00 == g0max);
+    sum += inv ? 0.f : srr;
+    ninv += inv ? 1.f : 0.f;
+    if (tru) {
+      const float l = inv ? 0.f : srr, n = inv ? 0.f : 1.f;
+      mn_all = fminf(mn_all, smin);
+      mx_all = fmaxf(mx_all, smax);
+      if (sr0 < mn0) { mn0 = sr0; lmn = l; nmn = n; } else if (sr0 == mn0) { lmn += l; nmn += n; }
+      if (sr0 > mx0) { mx0 = sr0; lmx = l; nmx = n; } else if (sr0 == mx0) { lmx += l; nmx += n; }
+    }
+  }
+  for (int off = 32; off > 0; off >>= 1) {
+    sum += __shfl_xor(sum, off);
+    ninv += __shfl_xor(ninv, off);
+    const float a0 = __shfl_xor(mn_all, off), a1 = __shfl_xor(mn0, off), a2 = __shfl_xor(lmn, off),
+                a3 = __shfl_xor(nmn, off);
+    mn_all = fminf(mn_all, a0);
+    if (a1 < mn0) { mn0 = a1; lmn = a2; nmn = a3; } else if (a1 == mn0) { lmn += a2; nmn += a3; }
+    const float b0 = __shfl_xor(mx_all, off), b1 = __shfl_xor(mx0, off), b2 = __shfl_xor(lmx, off),
+                b3 = __shfl_xor(nmx, off);
+    mx_all = fmaxf(mx_all, b0);
+    if (b1 > mx0) { mx0 = b1; lmx = b2; nmx = b3; } else if (b1 == mx0) { lmx += b2; nmx += b3; }
+  }
+  if (lane == 0) {
+    red[wave][L_SUM] = sum; red[wave][L_NINV] = ninv;
+    red[wave][L_MN_ALL] = mn_all; red[wave][L_MN0] = mn0; red[wave][L_LMN] = lmn; red[wave][L_NMN] = nmn;
+    red[wave][L_MX_ALL] = mx_all; red[wave][L_MX0] = mx0; red[wave][L_LMX] = lmx; red[wave][L_NMX] = nmx;
+  }
+  __syncthreads();
+  if (tid == 0) {
+    float* out = p.rec + (size_t)bid * kRec;
+    float s = red[0][L_SUM], ni = red[0][L_NINV];
+    float ma = red[0][L_MN_ALL], m0 = red[0][L_MN0], lm = red[0][L_LMN], nm = red[0][L_NMN];
+    float xa = red[0][L_MX_ALL], x0v = red[0][L_MX0], lx = red[0][L_LMX], nx = red[0][L_NMX];
+    for (int w = 1; w < 4; ++w) {
+      s += red[w][L_SUM];
+      ni += red[w][L_NINV];
+      ma = fminf(ma, red[w][L_MN_ALL]);
+      if (red[w][L_MN0] < m0) { m0 = red[w][L_MN0]; lm = red[w][L_LMN]; nm = red[w][L_NMN]; }
+      else if (red[w][L_MN0] == m0) { lm += red[w][L_LMN]; nm += red[w][L_NMN]; }
+      xa = fmaxf(xa, red[w][L_MX_ALL]);
+      if (red[w][L_MX0] > x0v) { x0v = red[w][L_MX0]; lx = red[w][L_LMX]; nx = red[w][L_NMX]; }
+      else if (red[w][L_MX0] == x0v) { lx += red[w][L_LMX]; nx += red[w][L_NMX]; }
+    }
+    out[L_SUM] = s; out[L_NINV] = ni;
+    out[L_MN_ALL] = ma; out[L_MN0] = m0; out[L_LMN] = lm; out[L_NMN] = nm;
+    out[L_MX_ALL] = xa; out[L_MX0] = x0v; out[L_LMX] = lx; out[L_NMX] = nx;
+  }
+}
+
+
+// ============================================================ per-pixel debug dump
+// out [B,5,H,W]: u, v, sigma_r (channel 0), sigma0 (channel 0), base-invalid
+// (occlusion | masks) as 0/1.  Test / debugging only (not on the solve path).
+__global__ __launch_bounds__(kThreads) void ic_debug_pixels_kernel(IterParams p, float* out) {
+  const int W = p.W, H = p.H, HW = H * W;
+  const int i = blockIdx.x * kThreads + threadIdx.x;
+  if (i >= p.B * HW) return;
+  const int b = i / HW, pix = i - b * HW, y = pix / W, x = pix - y * W;
+  const float fx = p.K[4 * b + 0], fy = p.K[4 * b + 1], cx = p.K[4 * b + 2], cy = p.K[4 * b + 3];
+  float Rm[9], tv[3];
+  for (int k = 0; k < 9; ++k) Rm[k] = p.R[9 * b + k];
+  for (int k = 0; k < 3; ++k) tv[k] = p.t[3 * b + k];
+  const float d = p.invD0[(size_t)b * HW + pix];
+  const Warp w = warp_point(x, y, d, Rm, tv, fx, fy, cx, cy);
+  PixelFrame px;
+  setup_pixel(p, b, x, y, d, Rm, tv, fx, fy, cx, cy, px);
+  float* o = out + (size_t)b * 5 * HW + pix;
+  o[0] = w.u;
+  o[HW] = w.v;
+  o[2 * HW] = bil(p.s1 + (size_t)b * p.Cs * HW, px.tp);
+  o[3 * HW] = p.s0[(size_t)b * p.Cs * HW + pix];
+  o[4 * HW] = px.invalid ? 1.0f : 0.0f;
+}
+
+// ============================================================ finalize
+struct FinParams {
+  const float* rec;
+  int nblocks, per_pair, HW;
+  uint32_t flags;
+  float* R;
+  float* t;
+  float* jtj_out;
+  float* jtr_out;
+  int32_t* invalid_out;
+  float* loss_out;
+  uint32_t* status;
+};
+
+__device__ __forceinline__ double wave_sum_d(double v) {
+  for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off);
+  return v;
+}
+
+// Global (whole-batch) extrema of sigma_r from every record.
+__device__ void global_extrema(const float* rec, int nblocks, int imn, int imx, float& gmin, float& gmax) {
+  __shared__ float sm[2][4];
+  float mn = INFINITY, mx = -INFINITY;
+  for (int k = threadIdx.x; k < nblocks; k += kThreads) {
+    mn = fminf(mn, rec[(size_t)k * kRec + imn]);
+    mx = fmaxf(mx, rec[(size_t)k * kRec + imx]);
+  }
+  for (int off = 32; off > 0; off >>= 1) {
+    mn = fminf(mn, __shfl_xor(mn, off));
+    mx = fmaxf(mx, __shfl_xor(mx, off));
+  }
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  if (lane == 0) {
+    sm[0][wave] = mn;
+    sm[1][wave] = mx;
+  }
+  __syncthreads();
+  gmin = fminf(fminf(sm[0][0], sm[0][1]), fminf(sm[0][2], sm[0][3]));
+  gmax = fmaxf(fmaxf(sm[1][0], sm[1][1]), fmaxf(sm[1][2], sm[1][3]));
+}
+
+// Solve (JtJ + 1e-6 tr(JtJ) I) xi = JtR in fp64 with partial pivoting and apply
+// the inverse-compositional update (algorithms.py:2035-2054, geometry.py:105-123,
+// 163-185): R <- R Exp(-w), t <- R (-Exp(-w) v) + t.
+__device__ void solve_and_update(const double* jtj_u, const double* jtr, float* Rp, float* tp) {
+  double A[6][7];
+  int k = 0;
+  for (int i = 0; i < 6; ++i)
+    for (int j = i; j < 6; ++j) {
+      A[i][j] = jtj_u[k];
+      A[j][i] = jtj_u[k];
+      ++k;
+    }
+  double tr = 0.0;
+  for (int i = 0; i < 6; ++i) tr += A[i][i];
+  for (int i = 0; i < 6; ++i) {
+    A[i][i] += 1e-6 * tr;
+    A[i][6] = jtr[i];
+  }
+  for (int c = 0; c < 6; ++c) {
+    int piv = c;
+    for (int r = c + 1; r < 6; ++r)
+      if (fabs(A[r][c]) > fabs(A[piv][c])) piv = r;
+    if (piv != c)
+      for (int j = 0; j < 7; ++j) {
+        const double tmp = A[c][j];
+        A[c][j] = A[piv][j];
+        A[piv][j] = tmp;
+      }
+    const double inv = 1.0 / A[c][c];
+    for (int r = c + 1; r < 6; ++r) {
+      const double f = A[r][c] * inv;
+      for (int j = c; j < 7; ++j) A[r][j] -= f * A[c][j];
+    }
+  }
+  double xi[6];
+  for (int i = 5; i >= 0; --i) {
+    double s = A[i][6];
+    for (int j = i + 1; j < 6; ++j) s -= A[i][j] * xi[j];
+    xi[i] = s / A[i][i];
+  }
+  // dR = Exp(-w): Rodrigues, NaN at |w| = 0 exactly as the reference.
+  const double w0 = -xi[0], w1 = -xi[1], w2 = -xi[2];
+  const double th = sqrt(w0 * w0 + w1 * w1 + w2 * w2);
+  const double k0 = w0 / th, k1 = w1 / th, k2 = w2 / th;
+  const double Kx[9] = {0.0, -k2, k1, k2, 0.0, -k0, -k1, k0, 0.0};
+  double KK[9];
+  for (int i = 0; i < 3; ++i)
+    for (int j = 0; j < 3; ++j) {
+      double s = 0.0;
+      for (int m = 0; m < 3; ++m) s += Kx[3 * i + m] * Kx[3 * m + j];
+      KK[3 * i + j] = s;
+    }
+  const double sn = sin(th), cs1 = 1.0 - cos(th);
+  double dR[9];
+  for (int i = 0; i < 9; ++i) dR[i] = ((i % 4 == 0) ? 1.0 : 0.0) + Kx[i] * sn + KK[i] * cs1;
+  double dt[3];
+  for (int i = 0; i < 3; ++i) dt[i] = -(dR[3 * i] * xi[3] + dR[3 * i + 1] * xi[4] + dR[3 * i + 2] * xi[5]);
+  double R0[9], t0[3];
+  for (int i = 0; i < 9; ++i) R0[i] = Rp[i];
+  for (int i = 0; i < 3; ++i) t0[i] = tp[i];
+  for (int i = 0; i < 3; ++i) {
+    for (int j = 0; j < 3; ++j) {
+      double s = 0.0;
+      for (int m = 0; m < 3; ++m) s += R0[3 * i + m] * dR[3 * m + j];
+      Rp[3 * i + j] = (float)s;
+    }
+    tp[i] = (float)(R0[3 * i] * dt[0] + R0[3 * i + 1] * dt[1] + R0[3 * i + 2] * dt[2] + t0[i]);
+  }
+}
+
+__global__ __launch_bounds__(kThreads) void ic_finalize_kernel(FinParams q) {
+  const int b = blockIdx.x;
+  const bool tru = (q.flags & DPFT_REMOVE_TRU_SIGMA) != 0;
+  float gmin = 0.f, gmax = 0.f;
+  if (tru) global_extrema(q.rec, q.nblocks, R_MN_ALL, R_MX_ALL, gmin, gmax);
+
+  double s[28];
+  for (int k = 0; k < 28; ++k) s[k] = 0.0;
+  const int first = b * q.per_pair;
+  for (int k = threadIdx.x; k < q.per_pair; k += kThreads) {
+    const float* r = q.rec + (size_t)(first + k) * kRec;
+    for (int i = 0; i < 28; ++i) s[i] += (double)r[i];
+    if (tru) {
+      if (r[R_MN0] == gmin) {
+        for (int i = 0; i < 6; ++i) s[21 + i] += (double)r[R_CMN + i];
+        s[27] += (double)r[R_NMN];
+      }
+      if (gmax != gmin && r[R_MX0] == gmax) {
+        for (int i = 0; i < 6; ++i) s[21 + i] += (double)r[R_CMX + i];
+        s[27] += (double)r[R_NMX];
+      }
+    }
+  }
+  __shared__ double sh[4][28];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  for (int i = 0; i < 28; ++i) {
+    const double v = wave_sum_d(s[i]);
+    if (lane == 0) sh[wave][i] = v;
+  }
+  __syncthreads();
+  if (threadIdx.x != 0) return;
+  double tot[28];
+  for (int i = 0; i < 28; ++i) tot[i] = ((sh[0][i] + sh[1][i]) + sh[2][i]) + sh[3][i];
+  bool finite = true;
+  for (int i = 0; i < 27; ++i) finite = finite && isfinite(tot[i]);
+  if (!finite && q.status) atomicOr(q.status, DPFT_STATUS_NONFINITE);
+  if (q.jtj_out) {
+    int k = 0;
+    for (int i = 0; i < 6; ++i)
+      for (int j = i; j < 6; ++j) {
+        q.jtj_out[36 * b + 6 * i + j] = (float)tot[k];
+        q.jtj_out[36 * b + 6 * j + i] = (float)tot[k];
+        ++k;
+      }
+  }
+  if (q.jtr_out)
+    for (int i = 0; i < 6; ++i) q.jtr_out[6 * b + i] = (float)tot[21 + i];
+  if (q.invalid_out) q.invalid_out[b] = (int32_t)tot[27];
+  solve_and_update(tot, tot + 21, q.R + 9 * b, q.t + 3 * b);
+}
+
+__global__ __launch_bounds__(kThreads) void ic_loss_finalize_kernel(FinParams q) {
+  const int b = blockIdx.x;
+  const bool tru = (q.flags & DPFT_REMOVE_TRU_SIGMA) != 0;
+  float gmin = 0.f, gmax = 0.f;
+  if (tru) global_extrema(q.rec, q.nblocks, L_MN_ALL, L_MX_ALL, gmin, gmax);
+  double sum = 0.0, ninv = 0.0;
+  const int first = b * q.per_pair;
+  for (int k = threadIdx.x; k < q.per_pair; k += kThreads) {
+    const float* r = q.rec + (size_t)(first + k) * kRec;
+    sum += r[L_SUM];
+    ninv += r[L_NINV];
+    if (tru) {
+      if (r[L_MN0] == gmin) { sum -= r[L_LMN]; ninv += r[L_NMN]; }
+      if (gmax != gmin && r[L_MX0] == gmax) { sum -= r[L_LMX]; ninv += r[L_NMX]; }
+    }
+  }
+  __shared__ double sh[2][4];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  sum = wave_sum_d(sum);
+  ninv = wave_sum_d(ninv);
+  if (lane == 0) {
+    sh[0][wave] = sum;
+    sh[1][wave] = ninv;
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    const double S = ((sh[0][0] + sh[0][1]) + sh[0][2]) + sh[0][3];
+    const double N = ((sh[1][0] + sh[1][1]) + sh[1][2]) + sh[1][3];
+    q.loss_out[b] = (float)(S / ((double)q.HW - N));
+  }
+}
+
+// sigma0 batch-global min / max (algorithms.py:1976-1977), order-preserving atomics.
+__global__ void ctrl_init_kernel(uint32_t* ctrl) {
+  ctrl[0] = 0xffffffffu;
+  ctrl[1] = 0u;
+}
+
+__global__ __launch_bounds__(kThreads) void minmax_kernel(const float* __restrict__ s, size_t n, uint32_t* ctrl) {
+  float mn = INFINITY, mx = -INFINITY;
+  const size_t stride = (size_t)gridDim.x * kThreads;
+  for (size_t i = (size_t)blockIdx.x * kThreads + threadIdx.x; i < n; i += stride) {
+    const float v = s[i];
+    mn = fminf(mn, v);
+    mx = fmaxf(mx, v);
+  }
+  for (int off = 32; off > 0; off >>= 1) {
+    mn = fminf(mn, __shfl_xor(mn, off));
+    mx = fmaxf(mx, __shfl_xor(mx, off));
+  }
+  if ((threadIdx.x & 63) == 0) {
+    atomicMin(&ctrl[0], enc_ord(mn));
+    atomicMax(&ctrl[1], enc_ord(mx));
+  }
+}
+
+// ------------------------------------------------------------------ host side
+struct Geometry {
+  int tiles_x, tiles_y, steps, nblocks, per_pair;
+};
+
+Geometry plan(const DpftLevelDesc& d) {
+  Geometry g;
+  g.tiles_x = (d.W + kTileW - 1) / kTileW;
+  const int row_groups = (d.H + kRowsPerStep - 1) / kRowsPerStep;
+  int steps = kMaxSteps;
+  // prefer >= 2048 workgroups (8 per CU) before taller tiles
+  while (steps > 1 && (long)g.tiles_x * ((row_groups + steps - 1) / steps) * d.B < 2048) steps >>= 1;
+  g.steps = steps;
+  g.tiles_y = (row_groups + steps - 1) / steps;
+  g.per_pair = g.tiles_x * g.tiles_y;
+  g.nblocks = g.per_pair * d.B;
+  return g;
+}
+
+int check_desc(const DpftLevelDesc* d) {
+  if (!d) return fail(DPFT_E_INVALID, "null descriptor");
+  if (d->B < 1 || d->C < 1 || d->H < 2 || d->W < 2)
+    return fail(DPFT_E_INVALID, "bad shape B=%d C=%d H=%d W=%d", d->B, d->C, d->H, d->W);
+  if (d->Cs != 1 && d->Cs != d->C) return fail(DPFT_E_INVALID, "Cs must be 1 or C (got %d, C=%d)", d->Cs, d->C);
+  if ((long)d->H * d->W >= (1L << 30)) return fail(DPFT_E_INVALID, "level too large");
+  if (d->flags & DPFT_COMBINE_ICP) return fail(DPFT_E_INVALID, "COMBINE_ICP not supported by this build yet");
+  return DPFT_OK;
+}
+
+int check_tensors(const DpftLevelTensors* t) {
+  if (!t || !t->f0 || !t->f1 || !t->s0 || !t->s1 || !t->invD0 || !t->invD1 || !t->K)
+    return fail(DPFT_E_INVALID, "null tensor pointer");
+  return DPFT_OK;
+}
+
+size_t ws_need(const DpftLevelDesc& d) {
+  const Geometry g = plan(d);
+  return kCtrlBytes + (size_t)g.nblocks * kRec * sizeof(float);
+}
+
+IterParams make_params(const DpftLevelDesc& d, const DpftLevelTensors& tt, const Geometry& g, const float* R,
+                       const float* t, void* ws) {
+  IterParams p;
+  p.f0 = tt.f0;
+  p.f1 = tt.f1;
+  p.s0 = tt.s0;
+  p.s1 = tt.s1;
+  p.invD0 = tt.invD0;
+  p.invD1 = tt.invD1;
+  p.mask0 = tt.mask0;
+  p.mask1 = tt.mask1;
+  p.K = tt.K;
+  p.R = R;
+  p.t = t;
+  p.B = d.B;
+  p.C = d.C;
+  p.Cs = d.Cs;
+  p.H = d.H;
+  p.W = d.W;
+  p.tiles_x = g.tiles_x;
+  p.tiles_y = g.tiles_y;
+  p.steps = g.steps;
+  p.nblocks = g.nblocks;
+  p.flags = d.flags;
+  p.ctrl = reinterpret_cast<const uint32_t*>(ws);
+  p.rec = reinterpret_cast<float*>(static_cast<char*>(ws) + kCtrlBytes);
+  return p;
+}
+
+int hip_check(const char* what) {
+  const hipError_t e = hipGetLastError();
+  if (e != hipSuccess) return fail(DPFT_E_HIP, "%s: %s", what, hipGetErrorString(e));
+  return DPFT_OK;
+}
+
+int launch_minmax(const DpftLevelDesc& d, const DpftLevelTensors& tt, void* ws, hipStream_t st) {
+  uint32_t* ctrl = reinterpret_cast<uint32_t*>(ws);
+  hipLaunchKernelGGL(ctrl_init_kernel, dim3(1), dim3(1), 0, st, ctrl);
+  if ((d.flags & DPFT_REMOVE_TRU_SIGMA) == 0) return hip_check("ctrl_init_kernel");
+  const size_t n = (size_t)d.B * d.Cs * d.H * d.W;
+  const int grid = (int)std::min<size_t>((n + kThreads * 4 - 1) / (kThreads * 4), 2048);
+  hipLaunchKernelGGL(minmax_kernel, dim3(grid), dim3(kThreads), 0, st, tt.s0, n, ctrl);
+  return hip_check("minmax_kernel");
+}
+
+template <int CT, bool CS1>
+void launch_reduce_t(const IterParams& p, hipStream_t st) {
+  if (p.flags & DPFT_REMOVE_TRU_SIGMA)
+    hipLaunchKernelGGL((ic_reduce_kernel<CT, CS1, true>), dim3(p.nblocks), dim3(kThreads), 0, st, p);
+  else
+    hipLaunchKernelGGL((ic_reduce_kernel<CT, CS1, false>), dim3(p.nblocks), dim3(kThreads), 0, st, p);
+}
+
+int launch_reduce(const IterParams& p, hipStream_t st) {
+  if (p.Cs == 1) {
+    switch (p.C) {
+      case 8: launch_reduce_t<8, true>(p, st); break;
+      case 16: launch_reduce_t<16, true>(p, st); break;
+      case 32: launch_reduce_t<32, true>(p, st); break;
+      default: launch_reduce_t<0, true>(p, st); break;
+    }
+  } else {
+    switch (p.C) {
+      case 8: launch_reduce_t<8, false>(p, st); break;
+      case 32: launch_reduce_t<32, false>(p, st); break;
+      default: launch_reduce_t<0, false>(p, st); break;
+    }
+  }
+  return hip_check("ic_reduce_kernel");
+}
+
+int iterate_impl(const DpftLevelDesc* desc, const DpftLevelTensors* tt, float* R, float* t, float* jtj_out,
+                 float* jtr_out, int32_t* invalid_out, int first, void* ws, size_t ws_bytes, hipStream_t st) {
+  int rc = check_desc(desc);
+  if (rc) return rc;
+  if ((rc = check_tensors(tt))) return rc;
+  if (!R || !t || !ws) return fail(DPFT_E_INVALID, "null pose / workspace");
+  if (ws_bytes < ws_need(*desc)) return fail(DPFT_E_WORKSPACE, "workspace %zu < %zu", ws_bytes, ws_need(*desc));
+  const Geometry g = plan(*desc);
+  if (first && (rc = launch_minmax(*desc, *tt, ws, st))) return rc;
+  const IterParams p = make_params(*desc, *tt, g, R, t, ws);
+  if ((rc = launch_reduce(p, st))) return rc;
+  FinParams q;
+  memset(&q, 0, sizeof(q));
+  q.rec = p.rec;
+  q.nblocks = g.nblocks;
+  q.per_pair = g.per_pair;
+  q.HW = desc->H * desc->W;
+  q.flags = desc->flags;
+  q.R = R;
+  q.t = t;
+  q.jtj_out = jtj_out;
+  q.jtr_out = jtr_out;
+  q.invalid_out = invalid_out;
+  q.status = tt->status;
+  hipLaunchKernelGGL(ic_finalize_kernel, dim3(desc->B), dim3(kThreads), 0, st, q);
+  return hip_check("ic_finalize_kernel");
+}
+
+}  // namespace
+
+extern "C" {
+
+size_t dpft_workspace_size(const DpftLevelDesc* desc) {
+  if (check_desc(desc)) return 0;
+  return ws_need(*desc);
+}
+
+int dpft_ic_iterate(const DpftLevelDesc* desc, const DpftLevelTensors* tensors, float* R, float* t, float* jtj_out,
+                    float* jtr_out, int32_t* invalid_out, int first, void* workspace, size_t workspace_bytes,
+                    void* hip_stream) {
+  return iterate_impl(desc, tensors, R, t, jtj_out, jtr_out, invalid_out, first, workspace, workspace_bytes,
+                      static_cast<hipStream_t>(hip_stream));
+}
+
+int dpft_ic_solve_level(const DpftLevelDesc* desc, const DpftLevelTensors* tensors, float* R, float* t,
+                        float* jtj_out, float* jtr_out, void* workspace, size_t workspace_bytes, void* hip_stream) {
+  int rc = check_desc(desc);
+  if (rc) return rc;
+  for (int it = 0; it < desc->iters; ++it) {
+    const bool last = it == desc->iters - 1;
+    rc = iterate_impl(desc, tensors, R, t, last ? jtj_out : nullptr, last ? jtr_out : nullptr, nullptr, it == 0,
+                      workspace, workspace_bytes, static_cast<hipStream_t>(hip_stream));
+    if (rc) return rc;
+  }
+  return DPFT_OK;
+}
+
+int dpft_ic_residual_level(const DpftLevelDesc* desc, const DpftLevelTensors* tt, const float* R, const float* t,
+                           float* loss, void* ws, size_t ws_bytes, void* hip_stream) {
+  int rc = check_desc(desc);
+  if (rc) return rc;
+  if ((rc = check_tensors(tt))) return rc;
+  if (!R || !t || !loss || !ws) return fail(DPFT_E_INVALID, "null pose / loss / workspace");
+  if (ws_bytes < ws_need(*desc)) return fail(DPFT_E_WORKSPACE, "workspace %zu < %zu", ws_bytes, ws_need(*desc));
+  hipStream_t st = static_cast<hipStream_t>(hip_stream);
+  const Geometry g = plan(*desc);
+  if ((rc = launch_minmax(*desc, *tt, ws, st))) return rc;
+  const IterParams p = make_params(*desc, *tt, g, R, t, ws);
+  if (p.Cs == 1)
+    hipLaunchKernelGGL(ic_residual_kernel<true>, dim3(p.nblocks), dim3(kThreads), 0, st, p);
+  else
+    hipLaunchKernelGGL(ic_residual_kernel<false>, dim3(p.nblocks), dim3(kThreads), 0, st, p);
+  if ((rc = hip_check("ic_residual_kernel"))) return rc;
+  FinParams q;
+  memset(&q, 0, sizeof(q));
+  q.rec = p.rec;
+  q.nblocks = g.nblocks;
+  q.per_pair = g.per_pair;
+  q.HW = desc->H * desc->W;
+  q.flags = desc->flags;
+  q.loss_out = loss;
+  q.status = tt->status;
+  hipLaunchKernelGGL(ic_loss_finalize_kernel, dim3(desc->B), dim3(kThreads), 0, st, q);
+  return hip_check("ic_loss_finalize_kernel");
+}
+
+int dpft_ic_reduce_only(const DpftLevelDesc* desc, const DpftLevelTensors* tt, const float* R, const float* t,
+                        void* ws, size_t ws_bytes, void* hip_stream) {
+  int rc = check_desc(desc);
+  if (rc) return rc;
+  if ((rc = check_tensors(tt))) return rc;
+  if (ws_bytes < ws_need(*desc)) return fail(DPFT_E_WORKSPACE, "workspace %zu < %zu", ws_bytes, ws_need(*desc));
+  const Geometry g = plan(*desc);
+  return launch_reduce(make_params(*desc, *tt, g, R, t, ws), static_cast<hipStream_t>(hip_stream));
+}
+
+int dpft_ic_debug_pixels(const DpftLevelDesc* desc, const DpftLevelTensors* tt, const float* R, const float* t,
+                         float* out, void* ws, size_t ws_bytes, void* hip_stream) {
+  int rc = check_desc(desc);
+  if (rc) return rc;
+  if ((rc = check_tensors(tt))) return rc;
+  if (!out || ws_bytes < ws_need(*desc)) return fail(DPFT_E_INVALID, "null output or small workspace");
+  const Geometry g = plan(*desc);
+  const IterParams p = make_params(*desc, *tt, g, R, t, ws);
+  const int n = desc->B * desc->H * desc->W;
+  hipLaunchKernelGGL(ic_debug_pixels_kernel, dim3((n + kThreads - 1) / kThreads), dim3(kThreads), 0,
+                     static_cast<hipStream_t>(hip_stream), p, out);
+  return hip_check("ic_debug_pixels_kernel");
+}
+
+int dpft_version(void) { return DPFT_ABI_VERSION; }
+
+const char* dpft_last_error(void) { return g_err; }
+
+}  // extern "C"

@@ -1,0 +1,210 @@
+"""Torch-facing entry points of the HIP solver (device tensors in, device tensors out).
+
+These are thin marshalling functions over libdpft_ic.so: they validate shapes,
+pick the uncertainty layout (Cs = 1 when sigma is a broadcast view or has one
+channel, Cs = C otherwise), hand raw device pointers and the caller's current
+HIP stream to the C ABI and never synchronise -- except `check_status`, which
+reads the device status word once (the reference asserts finiteness with a
+host sync every iteration, algorithms.py:886, 1988).
+
+Reference counterparts: `TrustRegionInverseWUncertainty.forward` /
+`forward_residuals` (code/models/algorithms.py:611-786).
+"""
+import ctypes
+
+import torch
+
+from . import _native as N
+
+_ws_cache = {}
+
+
+def _workspace(device, nbytes):
+    key = (device.type, device.index)
+    buf = _ws_cache.get(key)
+    if buf is None or buf.numel() < nbytes:
+        buf = torch.empty(max(nbytes, 1 << 20), dtype=torch.uint8, device=device)
+        _ws_cache[key] = buf
+    return buf
+
+
+def _ptr(t):
+    return ctypes.c_void_p(t.data_ptr()) if t is not None else ctypes.c_void_p(0)
+
+
+def _stream(device):
+    return ctypes.c_void_p(torch.cuda.current_stream(device).cuda_stream)
+
+
+def _sigma_planes(sigma, B, C, H, W):
+    """Return (tensor, Cs).  A channel-broadcast view ([B,1,H,W] expanded, stride 0)
+    or a single-channel tensor is passed with Cs=1 -- the reference's `.repeat`
+    (algorithms.py:1426-1427) carries no extra information."""
+    if sigma.dim() != 4 or sigma.shape[0] != B or sigma.shape[2:] != (H, W):
+        raise ValueError(f"sigma shape {tuple(sigma.shape)} incompatible with features [{B},{C},{H},{W}]")
+    if sigma.shape[1] == 1:
+        return sigma.contiguous(), 1
+    if sigma.shape[1] != C:
+        raise ValueError(f"sigma has {sigma.shape[1]} channels, expected 1 or {C}")
+    if sigma.stride(1) == 0:
+        return sigma[:, :1].contiguous(), 1
+    return sigma.contiguous(), C
+
+
+class LevelCall:
+    """Validated, pointer-ready arguments of one pyramid level."""
+
+    def __init__(self, x0, x1, invD0, invD1, K, sigma0, sigma1, iters=3, remove_tru_sigma=False,
+                 obj_mask0=None, obj_mask1=None, depth0=None, depth1=None, combine_icp=False,
+                 icp_weight=0.01, status=None):
+        if not x0.is_cuda:
+            raise RuntimeError("the HIP solver needs device tensors (got CPU); there is no CPU fallback")
+        for name, t in (("x0", x0), ("x1", x1), ("invD0", invD0), ("invD1", invD1), ("K", K)):
+            if t.dtype != torch.float32:
+                raise TypeError(f"{name} must be float32 (got {t.dtype})")
+            if t.device != x0.device:
+                raise ValueError(f"{name} is on {t.device}, expected {x0.device}")
+        B, C, H, W = x0.shape
+        if x1.shape != x0.shape:
+            raise ValueError(f"x1 {tuple(x1.shape)} != x0 {tuple(x0.shape)}")
+        for name, t in (("invD0", invD0), ("invD1", invD1)):
+            if tuple(t.shape) != (B, 1, H, W):
+                raise ValueError(f"{name} shape {tuple(t.shape)} != {(B, 1, H, W)}")
+        self.device = x0.device
+        self.x0, self.x1 = x0.contiguous(), x1.contiguous()
+        self.s0, cs0 = _sigma_planes(sigma0, B, C, H, W)
+        self.s1, cs1 = _sigma_planes(sigma1, B, C, H, W)
+        if cs0 != cs1:  # mixed layouts: fall back to full planes for both
+            self.s0, self.s1, cs0 = sigma0.expand(B, C, H, W).contiguous(), sigma1.expand(B, C, H, W).contiguous(), C
+        self.invD0, self.invD1 = invD0.contiguous(), invD1.contiguous()
+        self.K = K.reshape(B, 4).contiguous()
+        self.m0 = obj_mask0.reshape(B, 1, H, W).to(torch.uint8).contiguous() if obj_mask0 is not None else None
+        self.m1 = obj_mask1.reshape(B, 1, H, W).to(torch.uint8).contiguous() if obj_mask1 is not None else None
+        flags = N.REMOVE_TRU_SIGMA if remove_tru_sigma else 0
+        if combine_icp:
+            if depth0 is None or depth1 is None:
+                raise ValueError("combine_icp needs depth0 and depth1")
+            flags |= N.COMBINE_ICP
+        self.d0 = depth0.contiguous() if depth0 is not None else None
+        self.d1 = depth1.contiguous() if depth1 is not None else None
+        self.status = status if status is not None else torch.zeros(1, dtype=torch.int32, device=self.device)
+        self.desc = N.LevelDesc(B, C, cs0, H, W, iters, flags, icp_weight)
+        self.tens = N.LevelTensors(_ptr(self.x0), _ptr(self.x1), _ptr(self.s0), _ptr(self.s1), _ptr(self.invD0),
+                                   _ptr(self.invD1), _ptr(self.d0), _ptr(self.d1), _ptr(self.m0), _ptr(self.m1),
+                                   _ptr(self.K), _ptr(self.status))
+        self.B = B
+        nbytes = N.lib().dpft_workspace_size(ctypes.byref(self.desc))
+        if nbytes == 0:
+            N.check(-1, "dpft_workspace_size")
+        self.ws_bytes = nbytes
+        self.ws = _workspace(self.device, nbytes)
+
+    def pose_buffers(self, pose):
+        R, t = pose
+        R = R.to(torch.float32).reshape(self.B, 3, 3).contiguous().clone()
+        t = t.to(torch.float32).reshape(self.B, 3).contiguous().clone()
+        return R, t
+
+
+def check_status(status):
+    """Mirror of `assert check_nan(...) == 0` (algorithms.py:886, 1988): one host read."""
+    if int(status.item()) & N.STATUS_NONFINITE:
+        raise AssertionError("non-finite Jacobian / residual in the IC solver (reference: check_nan assert)")
+
+
+def solve_level(pose, x0, x1, invD0, invD1, K, sigma0, sigma1, iters=3, return_jtj=False, check=True, **kw):
+    """`iters` Gauss-Newton steps at one level; returns (R [B,3,3], t [B,3,1][, JtJ [B,6,6]])."""
+    c = LevelCall(x0, x1, invD0, invD1, K, sigma0, sigma1, iters=iters, **kw)
+    R, t = c.pose_buffers(pose)
+    jtj = torch.empty(c.B, 6, 6, dtype=torch.float32, device=c.device) if return_jtj else None
+    rc = N.lib().dpft_ic_solve_level(ctypes.byref(c.desc), ctypes.byref(c.tens), _ptr(R), _ptr(t), _ptr(jtj),
+                                     None, _ptr(c.ws), c.ws_bytes, _stream(c.device))
+    N.check(rc, "dpft_ic_solve_level")
+    if check:
+        check_status(c.status)
+    out = (R, t.view(c.B, 3, 1))
+    return out + (jtj,) if return_jtj else out
+
+
+def iterate(pose, x0, x1, invD0, invD1, K, sigma0, sigma1, first=True, **kw):
+    """One iteration; returns (R, t [B,3,1], JtJ [B,6,6], JtR [B,6], invalid [B]) -- test / trace API."""
+    c = LevelCall(x0, x1, invD0, invD1, K, sigma0, sigma1, iters=1, **kw)
+    R, t = c.pose_buffers(pose)
+    jtj = torch.empty(c.B, 6, 6, dtype=torch.float32, device=c.device)
+    jtr = torch.empty(c.B, 6, dtype=torch.float32, device=c.device)
+    inv = torch.empty(c.B, dtype=torch.int32, device=c.device)
+    rc = N.lib().dpft_ic_iterate(ctypes.byref(c.desc), ctypes.byref(c.tens), _ptr(R), _ptr(t), _ptr(jtj), _ptr(jtr),
+                                 _ptr(inv), int(bool(first)), _ptr(c.ws), c.ws_bytes, _stream(c.device))
+    N.check(rc, "dpft_ic_iterate")
+    return R, t.view(c.B, 3, 1), jtj, jtr, inv
+
+
+def residual_level(pose, x0, x1, invD0, invD1, K, sigma0, sigma1, **kw):
+    """forward_residuals: per-pair average loss [B] at a fixed pose."""
+    c = LevelCall(x0, x1, invD0, invD1, K, sigma0, sigma1, iters=1, **kw)
+    R, t = c.pose_buffers(pose)
+    loss = torch.empty(c.B, dtype=torch.float32, device=c.device)
+    rc = N.lib().dpft_ic_residual_level(ctypes.byref(c.desc), ctypes.byref(c.tens), _ptr(R), _ptr(t), _ptr(loss),
+                                        _ptr(c.ws), c.ws_bytes, _stream(c.device))
+    N.check(rc, "dpft_ic_residual_level")
+    return loss
+
+
+def debug_pixels(pose, x0, x1, invD0, invD1, K, sigma0, sigma1, **kw):
+    """Per-pixel dump [B,5,H,W] (u, v, sigma_r ch0, sigma0 ch0, occlusion|mask invalid) -- tests only."""
+    c = LevelCall(x0, x1, invD0, invD1, K, sigma0, sigma1, iters=1, **kw)
+    R, t = c.pose_buffers(pose)
+    out = torch.empty(c.B, 5, x0.shape[2], x0.shape[3], dtype=torch.float32, device=c.device)
+    rc = N.lib().dpft_ic_debug_pixels(ctypes.byref(c.desc), ctypes.byref(c.tens), _ptr(R), _ptr(t), _ptr(out),
+                                      _ptr(c.ws), c.ws_bytes, _stream(c.device))
+    N.check(rc, "dpft_ic_debug_pixels")
+    return out
+
+
+class PyramidSolver:
+    """Coarse-to-fine solve over prepared levels with fixed device buffers.
+
+    Mirrors `LeastSquareTracking.forward`'s level loop (LeastSquareTracking.py:349-445):
+    levels L-1 .. 0, K / 2^l, pose chained, `iters` steps per level.  All levels share
+    one workspace and one status word, and `run()` only enqueues kernels on the
+    current stream with fixed pointers, so it can be captured once into a HIP graph
+    and replayed.  `levels[l]` = dict(x0, x1, invD0, invD1, sigma0, sigma1[, obj_mask0,
+    obj_mask1, depth0, depth1]); K is the level-0 intrinsics [B,4].
+    """
+
+    def __init__(self, levels, K, iters=3, remove_tru_sigma=False, combine_icp=False, icp_weight=0.01):
+        dev = levels[0]["x0"].device
+        self.status = torch.zeros(1, dtype=torch.int32, device=dev)
+        self.calls = []
+        for l, d in enumerate(levels):
+            self.calls.append(LevelCall(d["x0"], d["x1"], d["invD0"], d["invD1"], (K / (2 ** l)).contiguous(),
+                                        d["sigma0"], d["sigma1"], iters=iters, remove_tru_sigma=remove_tru_sigma,
+                                        obj_mask0=d.get("obj_mask0"), obj_mask1=d.get("obj_mask1"),
+                                        depth0=d.get("depth0"), depth1=d.get("depth1"), combine_icp=combine_icp,
+                                        icp_weight=icp_weight, status=self.status))
+        nbytes = max(c.ws_bytes for c in self.calls)
+        self.ws = torch.empty(nbytes, dtype=torch.uint8, device=dev)  # private: safe to capture
+        self.ws_bytes = nbytes
+        self.device = dev
+        self.B = self.calls[0].B
+
+    def run(self, R, t):
+        """In place: R [B,3,3], t [B,3] fp32 contiguous device buffers."""
+        L = N.lib()
+        st = _stream(self.device)
+        for c in reversed(self.calls):
+            rc = L.dpft_ic_solve_level(ctypes.byref(c.desc), ctypes.byref(c.tens), _ptr(R), _ptr(t), None, None,
+                                       _ptr(self.ws), self.ws_bytes, st)
+            N.check(rc, "dpft_ic_solve_level")
+
+    def reduce_only(self, level, R, t):
+        """Launch only the fused residual/Jacobian/JtJ kernel of `level` (roofline timing)."""
+        c = self.calls[level]
+        rc = N.lib().dpft_ic_reduce_only(ctypes.byref(c.desc), ctypes.byref(c.tens), _ptr(R), _ptr(t),
+                                         _ptr(self.ws), self.ws_bytes, _stream(self.device))
+        N.check(rc, "dpft_ic_reduce_only")
+
+    def algorithmic_bytes(self, level):
+        """HBM bytes one reduce launch must read: P (2C + 2Cs + 2) fp32."""
+        d = self.calls[level].desc
+        return d.B * d.H * d.W * 4 * (2 * d.C + 2 * d.Cs + 2)

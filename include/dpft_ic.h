@@ -1,0 +1,143 @@
+/*
+ * dpft_ic.h -- C ABI of libdpft_ic.so, the MI355X (gfx950) implementation of the
+ * trust-region inverse-compositional (U_IC) solver hot path of
+ * Deep Probabilistic Feature-metric Tracking.
+ *
+ * Plain pointers and sizes only; every device pointer is caller-owned (torch
+ * caching allocator or hipMalloc).  The library never allocates, never
+ * synchronises the stream, and enqueues all work on the caller's stream, so
+ * every entry point can be captured into a hipGraph.
+ *
+ * Reference interfaces replaced (paths relative to the reference repo):
+ *   dpft_ic_solve_level    <- TrustRegionInverseWUncertainty.forward
+ *                             code/models/algorithms.py:611-723
+ *                             (+ precompute_jacobian_components 848-865,
+ *                                compute_inverse_residuals 1992-2015,
+ *                                compose_residuals 1960-1989,
+ *                                compose_inverse_jacobians 867-887,
+ *                                compute_jtj / compute_jtr 812-834,
+ *                                GN_solver -> lev_mar_H -> inverse_update_pose
+ *                                836-846, 2094-2103, 2035-2054)
+ *   dpft_ic_iterate        <- ONE pass of the loop body algorithms.py:646-693
+ *   dpft_ic_residual_level <- TrustRegionInverseWUncertainty.forward_residuals
+ *                             algorithms.py:725-786 (+ compute_avg_loss 2119-2137)
+ *   dpft_workspace_size / dpft_version / dpft_last_error: library plumbing.
+ *
+ * Semantics follow the reference exactly where they are observable:
+ *   - K is per pair [B,4] = (fx, fy, cx, cy) already divided by 2^level
+ *     (LeastSquareTracking.py:350: `K >> l` on a float tensor = K / 2^l);
+ *   - the truncated-sigma and invalid-normal masks use min / max over the whole
+ *     batch passed in one call (algorithms.py:1975-1980, 2168);
+ *   - the Jacobian is not masked; invalid pixels only get a weighted residual of
+ *     1e-6 (algorithms.py:867-887, 1982-1983);
+ *   - exactly `iters` Gauss-Newton steps, no early exit (algorithms.py:646);
+ *   - pose update R <- R Exp(-w), t <- R (-Exp(-w) v) + t (algorithms.py:2035-2054).
+ *
+ * Return codes: DPFT_OK, or a negative DPFT_E_* code; dpft_last_error() gives a
+ * thread-local message.  Non-finite Jacobians / residuals (the reference's
+ * `assert check_nan(...) == 0`, algorithms.py:886, 1988) are reported through
+ * the device status word (DPFT_STATUS_NONFINITE), read by the caller once per
+ * solve.
+ */
+#ifndef DPFT_IC_H
+#define DPFT_IC_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define DPFT_ABI_VERSION 1
+
+/* flags of DpftLevelDesc */
+#define DPFT_REMOVE_TRU_SIGMA 0x1u /* --remove_tru_sigma (algorithms.py:1975-1980) */
+#define DPFT_COMBINE_ICP      0x2u /* --combine_ICP (algorithms.py:668-689)        */
+
+/* device status word bits */
+#define DPFT_STATUS_NONFINITE 0x1u /* a JtJ / JtR reduction was not finite         */
+
+/* return codes */
+#define DPFT_OK            0
+#define DPFT_E_INVALID    -1 /* bad descriptor / null pointer / unsupported shape */
+#define DPFT_E_WORKSPACE  -2 /* workspace too small                                */
+#define DPFT_E_HIP        -3 /* a HIP runtime call failed                          */
+
+typedef struct DpftLevelDesc {
+    int32_t B;       /* pairs in the batch                                    */
+    int32_t C;       /* feature channels                                      */
+    int32_t Cs;      /* uncertainty channels: 1 (broadcast) or C              */
+    int32_t H, W;    /* level resolution                                      */
+    int32_t iters;   /* Gauss-Newton iterations (reference: max_iter_per_pyr)  */
+    uint32_t flags;  /* DPFT_REMOVE_TRU_SIGMA | DPFT_COMBINE_ICP              */
+    float icp_weight;/* ScaleNet('None') weight, 0.01 (algorithms.py:1563)    */
+} DpftLevelDesc;
+
+/* All tensors fp32 contiguous NCHW unless stated; nullable ones may be NULL. */
+typedef struct DpftLevelTensors {
+    const float* f0;      /* [B,C,H,W]  reference features                     */
+    const float* f1;      /* [B,C,H,W]  target features                        */
+    const float* s0;      /* [B,Cs,H,W] reference uncertainty                   */
+    const float* s1;      /* [B,Cs,H,W] target uncertainty                      */
+    const float* invD0;   /* [B,1,H,W]  reference inverse depth                 */
+    const float* invD1;   /* [B,1,H,W]  target inverse depth                    */
+    const float* depth0;  /* [B,1,H,W]  raw depth (COMBINE_ICP only)            */
+    const float* depth1;  /* [B,1,H,W]  raw depth (COMBINE_ICP only)            */
+    const uint8_t* mask0; /* [B,1,H,W]  object mask of frame 0, nullable        */
+    const uint8_t* mask1; /* [B,1,H,W]  object mask of frame 1, nullable        */
+    const float* K;       /* [B,4]      (fx,fy,cx,cy) of THIS level             */
+    uint32_t* status;     /* [1]        device status word, OR-ed, never cleared */
+} DpftLevelTensors;
+
+/* Bytes of workspace the level needs (>= 256-byte aligned pointer expected). */
+size_t dpft_workspace_size(const DpftLevelDesc* desc);
+
+/*
+ * Run desc->iters Gauss-Newton iterations at one pyramid level.
+ * R [B,3,3] (row-major) and t [B,3] are read and updated in place (fp32).
+ * jtj_out [B,36] / jtr_out [B,6] (nullable) receive the LAST iteration's
+ * undamped JtJ / JtR (the reference's `inv_sigma_ksi`, algorithms.py:716-721).
+ */
+int dpft_ic_solve_level(const DpftLevelDesc* desc, const DpftLevelTensors* tensors,
+                        float* R, float* t, float* jtj_out, float* jtr_out,
+                        void* workspace, size_t workspace_bytes, void* hip_stream);
+
+/*
+ * One iteration (residual -> Jacobian -> JtJ/JtR -> damped solve -> update).
+ * `first` must be non-zero on the first iteration of a level (it computes the
+ * per-level sigma0 extrema).  invalid_out [B] (nullable, int32) receives the
+ * number of invalid pixels of this iteration's residual.
+ */
+int dpft_ic_iterate(const DpftLevelDesc* desc, const DpftLevelTensors* tensors,
+                    float* R, float* t, float* jtj_out, float* jtr_out, int32_t* invalid_out,
+                    int first, void* workspace, size_t workspace_bytes, void* hip_stream);
+
+/*
+ * Residual-only evaluation at a fixed pose (forward_residuals):
+ * loss[b] = sum_valid sum_c w_res^2 [+ (w_icp r_icp)^2] / (H*W - #invalid).
+ */
+int dpft_ic_residual_level(const DpftLevelDesc* desc, const DpftLevelTensors* tensors,
+                           const float* R, const float* t, float* loss,
+                           void* workspace, size_t workspace_bytes, void* hip_stream);
+
+/* Kernel-only timing hook for the roofline: launch ONLY the fused residual +
+ * Jacobian + normal-equation kernel (no finalize), using the sigma0 extrema a
+ * previous dpft_ic_iterate(first=1) left in the workspace.  Used by bench.py. */
+int dpft_ic_reduce_only(const DpftLevelDesc* desc, const DpftLevelTensors* tensors,
+                        const float* R, const float* t,
+                        void* workspace, size_t workspace_bytes, void* hip_stream);
+
+/* Debug / test hook: per-pixel dump out[B,5,H,W] = (u, v, sigma_r ch0, sigma0 ch0,
+ * occlusion|mask invalid) at the given pose.  Not on the solve path. */
+int dpft_ic_debug_pixels(const DpftLevelDesc* desc, const DpftLevelTensors* tensors,
+                         const float* R, const float* t, float* out,
+                         void* workspace, size_t workspace_bytes, void* hip_stream);
+
+int dpft_version(void);            /* DPFT_ABI_VERSION */
+const char* dpft_last_error(void); /* thread-local message of the last failure */
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* DPFT_IC_H */

@@ -1,0 +1,217 @@
+"""HIP solver parity on a real MI355X (run with `-m gpu`).
+
+Every case compares libdpft_ic.so, called through the C ABI (ctypes), with
+  (a) the golden vectors produced by the reference itself (fp32 and fp64 runs),
+  (b) the CPU oracle on the same inputs.
+Tolerance (BASELINE.json north star): 1e-4 on every R and t entry (se(3)), per
+iteration and at the end; iteration counts are exact (3 per level, no early
+exit).  The reference's own fp32 noise floor is up to 9.7e-5 at 640x480 C=32
+(SURVEY.md App. B), so the fp64 golden run is the sharper check.
+"""
+import numpy as np
+import pytest
+import torch
+
+import golden_io
+import recipe
+
+pytestmark = pytest.mark.gpu
+
+SE3_TOL = 1e-4
+
+
+def _dev():
+    if not torch.cuda.is_available():
+        pytest.skip("no HIP device")
+    return torch.device("cuda:0")
+
+
+def _run_hip_trace(name, dev):
+    from deep_prob_feature_track_amd import ic
+    case, z = golden_io.load(name)
+    lv = golden_io.levels_torch(case, torch.float32, dev)
+    R, t = golden_io.init_pose(case, torch.float32, dev)
+    t = t.view(-1, 3, 1)
+    K = torch.from_numpy(case["K"]).to(dev)
+    trace = []
+    status = torch.zeros(1, dtype=torch.int32, device=dev)
+    for l in reversed(range(case["levels"])):
+        d = lv[l]
+        for it in range(3):
+            R, t, jtj, jtr, inv = ic.iterate(
+                (R, t), d["f0"], d["f1"], d["invD0"], d["invD1"], K / 2 ** l, d["s0"], d["s1"], first=(it == 0),
+                remove_tru_sigma=bool(z["opt_remove_tru_sigma"]), obj_mask0=d.get("mask0"),
+                obj_mask1=d.get("mask1"), depth0=d.get("depth0"), depth1=d.get("depth1"),
+                combine_icp=bool(z["opt_combine_icp"]), status=status)
+            trace.append(dict(R=R.cpu().numpy(), t=t.view(-1, 3).cpu().numpy(), jtj=jtj.cpu().numpy(),
+                              jtr=jtr.cpu().numpy(), invalid=inv.cpu().numpy()))
+    ic.check_status(status)
+    return case, z, trace
+
+
+FEATURE_CASES = ["cfg1_160x120_c8", "cfg1b_160x120_c8_f04", "batch4_160x120_c8", "masks_160x120_c8",
+                 "cfg2_640x480_c32"]
+
+
+@pytest.mark.parametrize("name", FEATURE_CASES)
+def test_hip_matches_reference_golden(name):
+    dev = _dev()
+    case, z, trace = _run_hip_trace(name, dev)
+    assert len(trace) == 3 * case["levels"]
+    for prec in ("f32", "f64"):
+        if f"{prec}_R" not in z:
+            continue
+        for i, tr in enumerate(trace):
+            dR = np.abs(tr["R"] - z[f"{prec}_R"][i]).max()
+            dt = np.abs(tr["t"] - z[f"{prec}_t"][i]).max()
+            assert dR <= SE3_TOL and dt <= SE3_TOL, f"{name} vs {prec} iter {i}: |dR|={dR:.2e} |dt|={dt:.2e}"
+    # first iteration: identical start pose and identical fp32 semantics -> the
+    # invalid set (occlusion, masks, truncated sigma) is the reference's bit for
+    # bit and the normal equations agree to accumulation-order rounding.
+    rel = np.abs(trace[0]["jtj"] - z["f32_jtj"][0]).max() / np.abs(z["f32_jtj"][0]).max()
+    assert rel < 1e-5, f"JtJ rel err {rel:.2e}"
+    relr = np.abs(trace[0]["jtr"] - z["f32_jtr"][0]).max() / np.abs(z["f32_jtr"][0]).max()
+    assert relr < 1e-4, f"JtR rel err {relr:.2e}"
+    assert (trace[0]["invalid"] == z["f32_invalid"][0]).all(), (trace[0]["invalid"], z["f32_invalid"][0])
+
+
+@pytest.mark.parametrize("name", ["cfg1_160x120_c8", "batch4_160x120_c8", "masks_160x120_c8"])
+def test_hip_residual_loss(name):
+    from deep_prob_feature_track_amd import ic
+    dev = _dev()
+    case, z = golden_io.load(name)
+    lv = golden_io.levels_torch(case, torch.float32, dev)
+    R, t = golden_io.init_pose(case, torch.float32, dev)
+    L = case["levels"]
+    d = lv[L - 1]
+    K = torch.from_numpy(case["K"]).to(dev) / 2 ** (L - 1)
+    loss = ic.residual_level((R, t), d["f0"], d["f1"], d["invD0"], d["invD1"], K, d["s0"], d["s1"],
+                             remove_tru_sigma=bool(z["opt_remove_tru_sigma"]), obj_mask0=d.get("mask0"),
+                             obj_mask1=d.get("mask1"))
+    np.testing.assert_allclose(loss.cpu().numpy(), z["f32_loss_start"][0], rtol=2e-5)
+
+
+def _random_case(B, C, Cs, H, W, seed, masks=False):
+    g = torch.Generator().manual_seed(seed)
+    f0 = torch.rand(B, C, H, W, generator=g)
+    # a smooth shifted copy so the solve has signal
+    f1 = torch.roll(f0, shifts=(1, 2), dims=(2, 3)) + 0.01 * torch.rand(B, C, H, W, generator=g)
+    s0 = 0.5 + torch.rand(B, Cs, H, W, generator=g)
+    s1 = 0.5 + torch.rand(B, Cs, H, W, generator=g)
+    invD0 = 0.2 + torch.rand(B, 1, H, W, generator=g)
+    invD1 = 0.2 + torch.rand(B, 1, H, W, generator=g)
+    K = torch.tensor([[W * 0.8, W * 0.8, (W - 1) / 2, (H - 1) / 2]]).repeat(B, 1)
+    m0 = (torch.rand(B, 1, H, W, generator=g) > 0.2) if masks else None
+    m1 = (torch.rand(B, 1, H, W, generator=g) > 0.2) if masks else None
+    return f0, f1, s0, s1, invD0, invD1, K, m0, m1
+
+
+@pytest.mark.parametrize("B,C,Cs,H,W,tru,masks", [
+    (1, 8, 1, 120, 160, True, False),
+    (2, 5, 1, 37, 70, True, True),      # ragged tiles, generic channel count
+    (3, 8, 8, 48, 64, True, False),     # per-channel uncertainty (Cs = C)
+    (2, 32, 1, 60, 80, False, False),
+    (1, 3, 3, 17, 129, False, True),
+])
+def test_hip_matches_oracle_random(B, C, Cs, H, W, tru, masks):
+    """HIP vs the fp32 CPU oracle on seeded random inputs, several shapes.
+
+    Same precision on both sides: the invalid set (u > 0 at column 0, z-test,
+    masks) is decided by the same fp32 bits, so iteration 0 must agree exactly
+    on it; an fp64 oracle would legitimately flip border pixels here."""
+    from deep_prob_feature_track_amd import ic
+    from oracle import ic_oracle as O
+    dev = _dev()
+    f0, f1, s0, s1, invD0, invD1, K, m0, m1 = _random_case(B, C, Cs, H, W, seed=B * 1000 + C * 10 + W, masks=masks)
+    R = torch.eye(3).repeat(B, 1, 1)
+    t = torch.zeros(B, 3, 1)
+    tr_o, tr_64 = [], []
+    O.solve_level(R, t, f0, f1, s0, s1, invD0, invD1, K, iters=3, remove_tru_sigma=tru, mask0=m0, mask1=m1,
+                  trace=tr_o)
+    dd = lambda a: a.double() if a is not None and a.dtype == torch.float32 else a
+    O.solve_level(dd(R), dd(t), dd(f0), dd(f1), dd(s0), dd(s1), dd(invD0), dd(invD1), dd(K), iters=1,
+                  remove_tru_sigma=tru, mask0=m0, mask1=m1, trace=tr_64)
+    cu = lambda a: a.to(dev) if a is not None else None
+    Rg, tg = R.to(dev), t.to(dev)
+    for it in range(3):
+        Rg, tg, jtj, jtr, inv = ic.iterate((Rg, tg), cu(f0), cu(f1), cu(invD0), cu(invD1), cu(K), cu(s0), cu(s1),
+                                           first=(it == 0), remove_tru_sigma=tru, obj_mask0=cu(m0),
+                                           obj_mask1=cu(m1))
+        ref = tr_o[it]
+        if it == 0:
+            # J is unmasked, so JtJ does not see the precision-dependent invalid set
+            rel = (jtj.cpu().double() - tr_64[0]["JtJ"]).abs().max() / tr_64[0]["JtJ"].abs().max()
+            assert rel < 1e-5, f"JtJ rel {rel:.2e}"
+            relr = (jtr.cpu() - ref["JtR"]).abs().max() / ref["JtR"].abs().max()
+            assert relr < 1e-4, f"JtR rel {relr:.2e}"
+            assert torch.equal(inv.cpu().long(), ref["invalid"].long())
+        dR = (Rg.cpu() - ref["R"]).abs().max().item()
+        dt = (tg.view(B, 3).cpu() - ref["t"]).abs().max().item()
+        assert dR <= SE3_TOL and dt <= SE3_TOL, f"iter {it}: |dR|={dR:.2e} |dt|={dt:.2e}"
+
+
+@pytest.mark.parametrize("name", ["cfg1_160x120_c8", "masks_160x120_c8", "batch4_160x120_c8", "cfg2_640x480_c32"])
+def test_invalid_mask_bit_exact(name):
+    """u, v, sigma_r and the occlusion / mask set equal the reference's fp32 CPU
+    arithmetic bit for bit at the start pose (tests/ref_arith.py emulates it
+    host-independently; pinned against torch by tests/test_ref_arith.py)."""
+    import ref_arith as A
+    from deep_prob_feature_track_amd import ic
+    dev = _dev()
+    case, z = golden_io.load(name)
+    L = case["levels"]
+    lvg = golden_io.levels_torch(case, torch.float32, dev)[L - 1]
+    R, t = golden_io.init_pose(case, torch.float32)
+    K = torch.from_numpy(case["K"]) / 2 ** (L - 1)
+    dbg = ic.debug_pixels((R.to(dev), t.to(dev)), lvg["f0"], lvg["f1"], lvg["invD0"], lvg["invD1"], K.to(dev),
+                          lvg["s0"], lvg["s1"], obj_mask0=lvg.get("mask0"), obj_mask1=lvg.get("mask1")).cpu().numpy()
+    lv = L - 1
+    for b in range(case["B"]):
+        H, W = case[f"invD0_{lv}"].shape[2:]
+        u, v, iz, _, _ = A.warp(H, W, case[f"invD0_{lv}"][b, 0], case["R_init"][b], case["t_init"][b], K[b].numpy())
+        occ = A.occlusion(u, v, iz, case[f"invD1_{lv}"][b, 0])
+        if f"mask0_{lv}" in case:
+            occ = occ | ~case[f"mask0_{lv}"][b, 0]
+        if f"mask1_{lv}" in case:
+            occ = occ | ~(A.sample(case[f"mask1_{lv}"][b].astype(np.float32), u, v)[0] > 0)
+        assert np.array_equal(dbg[b, 0], u) and np.array_equal(dbg[b, 1], v)
+        assert np.array_equal(dbg[b, 2], A.sample(case[f"s1_{lv}"][b], u, v)[0])
+        assert np.array_equal(dbg[b, 4].astype(bool), occ)
+
+
+def test_solve_level_equals_iterate():
+    """dpft_ic_solve_level (3 fused iterations) == 3 x dpft_ic_iterate, bit for bit."""
+    from deep_prob_feature_track_amd import ic
+    dev = _dev()
+    f0, f1, s0, s1, invD0, invD1, K, _, _ = [a.to(dev) if a is not None else None
+                                             for a in _random_case(2, 8, 1, 60, 80, seed=7)]
+    pose = (torch.eye(3, device=dev).repeat(2, 1, 1), torch.zeros(2, 3, 1, device=dev))
+    R1, t1 = ic.solve_level(pose, f0, f1, invD0, invD1, K, s0, s1, iters=3, remove_tru_sigma=True)
+    R2, t2 = pose
+    for it in range(3):
+        R2, t2, _, _, _ = ic.iterate((R2, t2), f0, f1, invD0, invD1, K, s0, s1, first=(it == 0),
+                                     remove_tru_sigma=True)
+    assert torch.equal(R1, R2) and torch.equal(t1, t2)
+
+
+def test_deterministic_repeat():
+    from deep_prob_feature_track_amd import ic
+    dev = _dev()
+    f0, f1, s0, s1, invD0, invD1, K, _, _ = [a.to(dev) if a is not None else None
+                                             for a in _random_case(4, 32, 1, 120, 160, seed=3)]
+    pose = (torch.eye(3, device=dev).repeat(4, 1, 1), torch.zeros(4, 3, 1, device=dev))
+    outs = [ic.solve_level(pose, f0, f1, invD0, invD1, K, s0, s1, iters=3, remove_tru_sigma=True) for _ in range(3)]
+    for R, t in outs[1:]:
+        assert torch.equal(R, outs[0][0]) and torch.equal(t, outs[0][1])
+
+
+def test_nonfinite_raises_assertion():
+    """sigma == 0 everywhere -> division by zero -> AssertionError like check_nan (algorithms.py:1988)."""
+    from deep_prob_feature_track_amd import ic
+    dev = _dev()
+    f0, f1, s0, s1, invD0, invD1, K, _, _ = [a.to(dev) if a is not None else None
+                                             for a in _random_case(1, 8, 1, 32, 64, seed=1)]
+    z = torch.zeros_like(s0)
+    pose = (torch.eye(3, device=dev)[None], torch.zeros(1, 3, 1, device=dev))
+    with pytest.raises(AssertionError):
+        ic.solve_level(pose, f0, f1, invD0, invD1, K, z, z, iters=1)
