@@ -54,10 +54,19 @@ namespace {
 constexpr int kThreads = 256;          // 4 waves of 64
 constexpr int kTileW = 64;             // one wave = 64 consecutive pixels of a row
 constexpr int kRowsPerStep = 4;        // one row per wave per step
-constexpr int kCK = 8;                 // channels staged in LDS per unit
+#ifndef DPFT_CK
+#define DPFT_CK 2
+#endif
+#ifndef DPFT_MAX_STEPS
+#define DPFT_MAX_STEPS 4
+#endif
+#ifndef DPFT_MIN_WAVES
+#define DPFT_MIN_WAVES 1
+#endif
+constexpr int kCK = DPFT_CK;           // channels staged in LDS per unit
 constexpr int kLdsW = kTileW + 2;      // 1-pixel halo each side
 constexpr int kLdsH = kRowsPerStep + 2;
-constexpr int kMaxSteps = 4;           // up to 16 rows per workgroup
+constexpr int kMaxSteps = DPFT_MAX_STEPS;  // up to 4 * kMaxSteps rows per workgroup
 
 // ---- reduce-record layout (floats) ------------------------------------------
 constexpr int kRec = 48;
@@ -244,6 +253,11 @@ __device__ __forceinline__ void sobel_lds(const float* __restrict__ L, int r, in
   ctr = v11;
 }
 
+// Same, on a 3-row stencil window (rows 0..2, centre row 1).
+__device__ __forceinline__ void sobel_lds_w(const float* __restrict__ L, int c, float& gx, float& gy, float& ctr) {
+  sobel_lds(L, 1, c, gx, gy, ctr);
+}
+
 // Warp Jacobian at the origin, xi = [rot, trs] (algorithms.py:1908-1917).
 __device__ __forceinline__ void warp_jac(float xr, float yr, float d, float fx, float fy, float* Jx, float* Jy) {
   const float xy = xr * yr;
@@ -298,84 +312,70 @@ __device__ __forceinline__ void ext_wave_reduce(Extremum& e) {
   }
 }
 
-// ---------------------------------------------------------------- LDS staging
-// A stage unit = one step (4 image rows + 1 halo row above and below) x one
-// chunk of <= kCK channels of f0, plus sigma0 (its single plane at chunk 0 when
-// Cs == 1, the chunk's planes otherwise).  The unit is a list of "rows": row q
-// is plane-row (q % 6) of the q/6-th staged plane.  Wave w loads rows w, w+4,
-// ...: one 64-lane load per row (LDS cols 0..63 = image cols x0-1 .. x0+62,
-// clamped = replicate padding) plus ONE load per wave for all its rows' right
-// halo (cols 64, 65).  Addresses are a scalar row base plus a fixed per-lane
-// column, so the loads cost no vector ALU; they are issued one unit ahead into
-// registers and written to the other LDS buffer after the current unit's math.
-template <bool CS1>
-struct StageCfg {
-  static constexpr int kPlanes = CS1 ? kCK + 1 : 2 * kCK;  // max planes per unit
-  static constexpr int kRows = kPlanes * kLdsH;            // max rows per unit
-  static constexpr int kRowsPerWave = (kRows + 3) / 4;
-  static constexpr int kBufFloats = kRows * kLdsW;
+// ---------------------------------------------------------------- buffer loads
+// Raw buffer loads: a scalar resource per tensor plane-set, a per-lane byte
+// offset that is fixed per pixel (or per tile column) and a scalar offset per
+// channel / row -- no vector ALU spent on addresses, and any offset past the
+// plane set reads 0 instead of faulting.
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t rsrc(const void* p, uint32_t bytes) {
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(p), (short)0, (int)bytes, 0x00020000);
+}
+__device__ __forceinline__ float bld(__amdgpu_buffer_rsrc_t r, int voff, int soff) {
+  return __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(r, voff, soff, 0));
+}
+
+struct Gather4 {
+  float a, b, c, d;
 };
+__device__ __forceinline__ Gather4 gather4(__amdgpu_buffer_rsrc_t r, const Taps& t, int soff) {
+  Gather4 g;
+  g.a = bld(r, t.o00 * 4, soff);
+  g.b = bld(r, t.o01 * 4, soff);
+  g.c = bld(r, t.o10 * 4, soff);
+  g.d = bld(r, t.o11 * 4, soff);
+  return g;
+}
 
-struct UnitGeom {
-  int c0, nc, nplanes, y0;  // nplanes = f0 planes + sigma0 planes staged in this unit
+// ---------------------------------------------------------------- stencil by DPP
+// No LDS and no workgroup barrier on the hot loop.  A wave owns one image row per
+// step; lane l holds image column x0 - 1 + l (clamped = replicate padding), so a
+// tile is 62 output pixels wide and lanes 0 and 63 only carry the halo.  Per
+// channel every lane loads its own column in rows y-1, y, y+1 (three coalesced
+// 256-byte loads) and forms the separable Sobel: V = top + 2 mid + bottom,
+// D = bottom - top, gx = V(l+1) - V(l-1), gy = D(l-1) + 2 D(l) + D(l+1), the
+// neighbour columns coming from DPP wave_shr:1 / wave_shl:1 lane shifts.
+constexpr int kTileOut = kTileW - 2;  // output pixels per tile row
+
+__device__ __forceinline__ float lane_from_left(float v) {  // lane l gets lane l - 1
+  return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x138, 0xf, 0xf, false));
+}
+__device__ __forceinline__ float lane_from_right(float v) {  // lane l gets lane l + 1
+  return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x130, 0xf, 0xf, false));
+}
+
+// Unit-normalised Sobel from the three rows of this lane's column (algorithms.py:1852-1863).
+__device__ __forceinline__ void sobel_cols(float top, float mid, float bot, float& gx, float& gy) {
+  const float V = top + 2.0f * mid + bot;
+  const float D = bot - top;
+  const float x = lane_from_right(V) - lane_from_left(V);
+  const float y = (lane_from_left(D) + 2.0f * D) + lane_from_right(D);
+  const float inv = rsqrtf(x * x + y * y + 1e-8f);
+  gx = x * inv;
+  gy = y * inv;
+}
+
+struct ChanLoads {
+  float t, m, b;  // f0 column in rows y-1, y, y+1
+  Gather4 g;      // f1 taps
 };
-
-// plane p of a unit -> source pointer
-template <bool CS1>
-__device__ __forceinline__ const float* plane_src(const float* f0b, const float* s0b, int HW, const UnitGeom& g,
-                                                  int pidx) {
-  if (pidx < g.nc) return f0b + (size_t)(g.c0 + pidx) * HW;
-  const int sp = pidx - g.nc;
-  return s0b + (size_t)(CS1 ? 0 : g.c0 + sp) * HW;
-}
-
-template <bool CS1>
-__device__ __forceinline__ void stage_load(float (&reg)[StageCfg<CS1>::kRowsPerWave], float& halo,
-                                           const float* f0b, const float* s0b, const UnitGeom& g, int H, int W,
-                                           int x0, int wave, int lane) {
-  const int HW = H * W;
-  const int nrows = g.nplanes * kLdsH;
-  const int col = min(max(x0 - 1 + lane, 0), W - 1);
-#pragma unroll
-  for (int j = 0; j < StageCfg<CS1>::kRowsPerWave; ++j) {
-    const int q = wave + 4 * j;  // wave-uniform
-    if (q < nrows) {
-      const int pl = q / kLdsH, r = q - pl * kLdsH;
-      const int gy = min(max(g.y0 - 1 + r, 0), H - 1);
-      reg[j] = plane_src<CS1>(f0b, s0b, HW, g, pl)[gy * W + col];
-    }
-  }
-  // right halo of every row of this wave: lane l -> row j = l >> 1, col 64 + (l & 1)
-  const int j = lane >> 1;
-  const int q = wave + 4 * j;
-  if (j < StageCfg<CS1>::kRowsPerWave && q < nrows) {
-    const int pl = q / kLdsH, r = q - pl * kLdsH;
-    const int gy = min(max(g.y0 - 1 + r, 0), H - 1);
-    const int hc = min(x0 + 63 + (lane & 1), W - 1);
-    halo = plane_src<CS1>(f0b, s0b, HW, g, pl)[gy * W + hc];
-  }
-}
-
-template <bool CS1>
-__device__ __forceinline__ void stage_store(float* __restrict__ buf, const float (&reg)[StageCfg<CS1>::kRowsPerWave],
-                                            float halo, const UnitGeom& g, int wave, int lane) {
-  const int nrows = g.nplanes * kLdsH;
-#pragma unroll
-  for (int j = 0; j < StageCfg<CS1>::kRowsPerWave; ++j) {
-    const int q = wave + 4 * j;
-    if (q < nrows) buf[q * kLdsW + lane] = reg[j];
-  }
-  const int j = lane >> 1;
-  const int q = wave + 4 * j;
-  if (j < StageCfg<CS1>::kRowsPerWave && q < nrows) buf[q * kLdsW + 64 + (lane & 1)] = halo;
-}
 
 // ============================================================ fused reduce kernel
+// Loads of channel chunk k+1 are issued before chunk k's math; chunks go in
+// (even, odd) pairs so each load set lives in fixed registers and no in-flight
+// load is ever copied (a copy would force the wait the prefetch exists to avoid).
 template <int CT, bool CS1, bool TRU>
-__global__ __launch_bounds__(kThreads) void ic_reduce_kernel(IterParams p) {
-  using SC = StageCfg<CS1>;
+__global__ __launch_bounds__(kThreads, DPFT_MIN_WAVES) void ic_reduce_kernel(IterParams p) {
   const int C = CT > 0 ? CT : p.C;
-  __shared__ float lds_buf[2][SC::kBufFloats];
   __shared__ float lds_ext[TRU ? 2 * 7 : 1][kThreads];  // extremum corrections (6 + count), min then max
   __shared__ float red[4][kRec];
 
@@ -395,11 +395,15 @@ __global__ __launch_bounds__(kThreads) void ic_reduce_kernel(IterParams p) {
   for (int k = 0; k < 3; ++k) tv[k] = p.t[3 * b + k];
   const float g0min = TRU ? dec_ord(p.ctrl[0]) : 0.f, g0max = TRU ? dec_ord(p.ctrl[1]) : 0.f;
 
-  const float* f0b = p.f0 + (size_t)b * C * HW;
-  const float* f1b = p.f1 + (size_t)b * C * HW;
-  const float* s0b = p.s0 + (size_t)b * p.Cs * HW;
-  const float* s1b = p.s1 + (size_t)b * p.Cs * HW;
-  const float* d0b = p.invD0 + (size_t)b * HW;
+  const uint32_t planeB = (uint32_t)HW * 4u;
+  const auto rf0 = rsrc(p.f0 + (size_t)b * C * HW, planeB * C);
+  const auto rf1 = rsrc(p.f1 + (size_t)b * C * HW, planeB * C);
+  const auto rs0 = rsrc(p.s0 + (size_t)b * p.Cs * HW, planeB * p.Cs);
+  const auto rs1 = rsrc(p.s1 + (size_t)b * p.Cs * HW, planeB * p.Cs);
+  const auto rd0 = rsrc(p.invD0 + (size_t)b * HW, planeB);
+  const auto rd1 = rsrc(p.invD1 + (size_t)b * HW, planeB);
+  const uint8_t* m0b = p.mask0 ? p.mask0 + (size_t)b * HW : nullptr;
+  const uint8_t* m1b = p.mask1 ? p.mask1 + (size_t)b * HW : nullptr;
 
   float acc[27];
 #pragma unroll
@@ -411,169 +415,168 @@ __global__ __launch_bounds__(kThreads) void ic_reduce_kernel(IterParams p) {
     for (int k = 0; k < 14; ++k) lds_ext[k][tid] = 0.0f;
   }
 
-  const int x0 = tx * kTileW;
-  const int x = x0 + lane;
+  const int xs = tx * kTileOut - 1 + lane;          // this lane's image column (may be -1 or >= W)
+  const int xc = min(max(xs, 0), W - 1);            // clamped: replicate padding of the stencil
+  const bool out_lane = (lane >= 1) && (lane <= kTileOut) && (xs < W);
+  const int colv = xc * 4;
   const int nch = (C + kCK - 1) / kCK;
-  int nsteps = p.steps;
-  {
-    const int last_row = (ty * p.steps + nsteps) * kRowsPerStep;  // steps fully below the image: skip
-    const int over = last_row - H;
-    if (over >= kRowsPerStep) nsteps -= over / kRowsPerStep;
-  }
-  auto unit_geom = [&](int s, int k) {
-    UnitGeom g;
-    g.c0 = k * kCK;
-    g.nc = min(kCK, C - g.c0);
-    g.nplanes = g.nc + (CS1 ? (k == 0 ? 1 : 0) : g.nc);
-    g.y0 = (ty * p.steps + s) * kRowsPerStep;
-    return g;
-  };
+  const int npair = (nch + 1) >> 1;                 // chunk pairs per step (odd counts get an empty chunk)
+  const int yb = ty * p.steps * kRowsPerStep;
 
-  float reg[SC::kRowsPerWave];
-  float halo = 0.0f;
-  {
-    const UnitGeom g0 = unit_geom(0, 0);
-    stage_load<CS1>(reg, halo, f0b, s0b, g0, H, W, x0, wave, lane);
-    stage_store<CS1>(lds_buf[0], reg, halo, g0, wave, lane);
-  }
-  float d_next = 0.0f;
-  {
-    const int y = (ty * p.steps) * kRowsPerStep + wave;
-    if (x < W && y < H) d_next = d0b[y * W + x];
-  }
-  __syncthreads();
+  float d_cur = bld(rd0, min(yb + wave, H - 1) * W * 4 + colv, 0);
+  for (int s = 0; s < p.steps; ++s) {
+    const int y = yb + s * kRowsPerStep + wave;
+    if (__builtin_amdgcn_readfirstlane(y) >= H) break;  // wave-uniform: this wave's rows are done
+    const int rT = max(y - 1, 0) * W * 4, rM = y * W * 4, rB = min(y + 1, H - 1) * W * 4;
+    // ---- frame: warp, taps, occlusion, masks (geometry.py:291-350, algorithms.py:1999-2008)
+    const float d = d_cur;
+    const Warp wp = warp_point(xc, y, d, Rm, tv, fx, fy, cx, cy);
+    const Taps tp = make_taps(wp.u, wp.v, H, W);
+    const Gather4 gd1 = gather4(rd1, tp, 0);
+    const bool m0 = m0b ? (m0b[y * W + xc] != 0) : true;
+    const float m1 = m1b ? bil_u8(m1b, tp) : 1.0f;
+    float s0t = 0.f, s0m = 0.f, s0b_ = 0.f;
+    Gather4 gs1;
+    if (CS1) {
+      s0t = bld(rs0, colv, rT);
+      s0m = bld(rs0, colv, rM);
+      s0b_ = bld(rs0, colv, rB);
+      gs1 = gather4(rs1, tp, 0);
+    }
+    if (s + 1 < p.steps) d_cur = bld(rd0, min(y + kRowsPerStep, H - 1) * W * 4 + colv, 0);
 
-  int u = 0;
-  for (int s = 0; s < nsteps; ++s) {
-    const int y = (ty * p.steps + s) * kRowsPerStep + wave;
-    const bool active = (x < W) && (y < H);
-    PixelFrame px;
-    px.invalid = true;
-    const float d = d_next;
-    if (active) setup_pixel(p, b, x, y, d, Rm, tv, fx, fy, cx, cy, px);
-    if (s + 1 < nsteps) {
-      const int yn = y + kRowsPerStep;
-      if (x < W && yn < H) d_next = d0b[yn * W + x];
+    ChanLoads LE[kCK], LO[kCK];
+    auto issue = [&](ChanLoads (&L)[kCK], int k) {
+#pragma unroll
+      for (int cc = 0; cc < kCK; ++cc) {
+        const int c = k * kCK + cc;
+        if (c < C) {
+          const int po = c * (int)planeB;
+          L[cc].t = bld(rf0, colv, po + rT);
+          L[cc].m = bld(rf0, colv, po + rM);
+          L[cc].b = bld(rf0, colv, po + rB);
+          L[cc].g = gather4(rf1, tp, po);
+        }
+      }
+    };
+    issue(LE, 0);
+
+    bool invalid;
+    {
+      const float d1w = bil4(gd1.a, gd1.b, gd1.c, gd1.d, tp);
+      const bool ok = (wp.iz > d1w - 0.1f) && (wp.u > 0.0f) && (wp.u < (float)W) && (wp.v > 0.0f) &&
+                      (wp.v < (float)H);
+      invalid = !ok || !out_lane || !m0 || !(m1 > 0.0f);
+    }
+    float sr0 = 0.f, srmin = 0.f, srmax = 0.f, inv_s = 0.f, kk = 0.f, hx = 0.f, hy = 0.f;
+    if (CS1) {
+      sobel_cols(s0t, s0m, s0b_, hx, hy);
+      sr0 = bil4(gs1.a, gs1.b, gs1.c, gs1.d, tp);
+      srmin = srmax = sr0;
+      const float sg = sqrtf(sr0 * sr0 + s0m * s0m);
+      inv_s = 1.0f / sg;
+      kk = s0m * (inv_s * inv_s * inv_s);
+      if (TRU) invalid = invalid || (s0m == g0min) || (s0m == g0max);
     }
     float Saa = 0.f, Sab = 0.f, Sbb = 0.f, Sa = 0.f, Sb = 0.f, Sar = 0.f, Sbr = 0.f;
 
-    for (int k = 0; k < nch; ++k, ++u) {
-      const UnitGeom g = unit_geom(s, k);
-      // issue the next unit's loads first: they fly while this unit computes
-      const bool has_next = (k + 1 < nch) || (s + 1 < nsteps);
-      UnitGeom gn = g;
-      if (has_next) {
-        gn = (k + 1 < nch) ? unit_geom(s, k + 1) : unit_geom(s + 1, 0);
-        stage_load<CS1>(reg, halo, f0b, s0b, gn, H, W, x0, wave, lane);
-      }
-      const float* buf = lds_buf[u & 1];
-      const float* sbuf = buf + g.nc * kLdsH * kLdsW;  // sigma0 planes follow the f0 planes
-      if (active) {
-        if (CS1 && k == 0) {
-          float ctr;
-          sobel_lds(sbuf, wave + 1, lane + 1, px.hx, px.hy, ctr);
-          px.sr0 = bil(s1b, px.tp);
-          px.srmin = px.srmax = px.sr0;
-          const float sg = sqrtf(px.sr0 * px.sr0 + ctr * ctr);
-          px.inv_s = 1.0f / sg;
-          px.kk = ctr * (px.inv_s * px.inv_s * px.inv_s);
-          if (TRU) px.invalid = px.invalid || (ctr == g0min) || (ctr == g0max);
-        }
+    auto unit = [&](int k, ChanLoads (&cur)[kCK], ChanLoads (&nxt)[kCK]) {
+      if (k + 1 < 2 * npair) issue(nxt, k + 1);
 #pragma unroll
-        for (int cc = 0; cc < kCK; ++cc) {
-          if (CT == 0 && cc >= g.nc) break;
-          if (CT > 0 && (CT % kCK) != 0 && cc >= g.nc) break;
-          const int c = g.c0 + cc;
-          float gx, gy, f0v;
-          sobel_lds(buf + cc * kLdsH * kLdsW, wave + 1, lane + 1, gx, gy, f0v);
-          float inv_s, kk, hx, hy;
-          if (CS1) {
-            inv_s = px.inv_s;
-            kk = px.kk;
-            hx = px.hx;
-            hy = px.hy;
+      for (int cc = 0; cc < kCK; ++cc) {
+        const int c = k * kCK + cc;
+        if (c >= C) break;
+        float gx, gy;
+        sobel_cols(cur[cc].t, cur[cc].m, cur[cc].b, gx, gy);
+        const float f0v = cur[cc].m;
+        float is_c = inv_s, kk_c = kk, hx_c = hx, hy_c = hy;
+        if (!CS1) {
+          const int po = c * (int)planeB;
+          const float st_ = bld(rs0, colv, po + rT), sm_ = bld(rs0, colv, po + rM), sb_ = bld(rs0, colv, po + rB);
+          sobel_cols(st_, sm_, sb_, hx_c, hy_c);
+          const float src = bil(p.s1 + ((size_t)b * p.Cs + c) * HW, tp);
+          const float sg = sqrtf(src * src + sm_ * sm_);
+          is_c = 1.0f / sg;
+          kk_c = sm_ * (is_c * is_c * is_c);
+          if (c == 0) {
+            sr0 = src;
+            srmin = srmax = src;
+            if (TRU) invalid = invalid || (sm_ == g0min) || (sm_ == g0max);
           } else {
-            float s0c;
-            sobel_lds(sbuf + cc * kLdsH * kLdsW, wave + 1, lane + 1, hx, hy, s0c);
-            const float src = bil(s1b + (size_t)c * HW, px.tp);
-            const float sg = sqrtf(src * src + s0c * s0c);
-            inv_s = 1.0f / sg;
-            kk = s0c * (inv_s * inv_s * inv_s);
-            if (c == 0) {
-              px.sr0 = src;
-              px.srmin = px.srmax = src;
-              if (TRU) px.invalid = px.invalid || (s0c == g0min) || (s0c == g0max);
-            } else {
-              px.srmin = fminf(px.srmin, src);
-              px.srmax = fmaxf(px.srmax, src);
-            }
+            srmin = fminf(srmin, src);
+            srmax = fmaxf(srmax, src);
           }
-          const float fr = bil(f1b + (size_t)c * HW, px.tp);
-          const float r = fr - f0v;
-          const float rw = r * inv_s;
-          const float rk = r * kk;
-          const float a = -(gx * inv_s + rk * hx);
-          const float bq = -(gy * inv_s + rk * hy);
-          Saa += a * a;
-          Sab += a * bq;
-          Sbb += bq * bq;
-          Sa += a;
-          Sb += bq;
-          Sar += a * rw;
-          Sbr += bq * rw;
+        }
+        const float frv = bil4(cur[cc].g.a, cur[cc].g.b, cur[cc].g.c, cur[cc].g.d, tp);
+        const float r = frv - f0v;
+        const float rw = r * is_c;
+        const float rk = r * kk_c;
+        const float a = -(gx * is_c + rk * hx_c);
+        const float bq = -(gy * is_c + rk * hy_c);
+        Saa += a * a;
+        Sab += a * bq;
+        Sbb += bq * bq;
+        Sa += a;
+        Sb += bq;
+        Sar += a * rw;
+        Sbr += bq * rw;
+      }
+    };
+
+#pragma unroll 1
+    for (int kp = 0; kp < npair; ++kp) {
+      unit(2 * kp, LE, LO);
+      unit(2 * kp + 1, LO, LE);
+    }
+
+    if (out_lane) {
+      float Jx[6], Jy[6];
+      warp_jac(wp.xr, wp.yr, d, fx, fy, Jx, Jy);
+      // weighted residual of invalid pixels is 1e-6 on every channel (algorithms.py:1982-1983)
+      const float cA = invalid ? 1e-6f * Sa : Sar;
+      const float cB = invalid ? 1e-6f * Sb : Sbr;
+      float P[6], Q[6];
+#pragma unroll
+      for (int i = 0; i < 6; ++i) {
+        P[i] = Saa * Jx[i] + Sab * Jy[i];
+        Q[i] = Sab * Jx[i] + Sbb * Jy[i];
+      }
+      int kq = 0;
+#pragma unroll
+      for (int i = 0; i < 6; ++i) {
+#pragma unroll
+        for (int j = i; j < 6; ++j) {
+          acc[kq] += P[i] * Jx[j] + Q[i] * Jy[j];
+          ++kq;
         }
       }
-      if (has_next) stage_store<CS1>(lds_buf[(u + 1) & 1], reg, halo, gn, wave, lane);
-      __syncthreads();
-    }
-    if (!active) continue;
+#pragma unroll
+      for (int i = 0; i < 6; ++i) acc[21 + i] -= cA * Jx[i] + cB * Jy[i];
+      ninv += invalid ? 1.0f : 0.0f;
 
-    float Jx[6], Jy[6];
-    warp_jac(px.xr, px.yr, px.d, fx, fy, Jx, Jy);
-    // weighted residual of invalid pixels is 1e-6 on every channel (algorithms.py:1982-1983)
-    const float cA = px.invalid ? 1e-6f * Sa : Sar;
-    const float cB = px.invalid ? 1e-6f * Sb : Sbr;
-    float P[6], Q[6];
+      if (TRU) {
+        mn_all = fminf(mn_all, srmin);
+        mx_all = fmaxf(mx_all, srmax);
+        const bool le = sr0 <= mn0, ge = sr0 >= mx0;
+        if (le || ge) {
+          float corr[7];
+          const float dA = invalid ? 0.0f : (1e-6f * Sa - Sar);
+          const float dB = invalid ? 0.0f : (1e-6f * Sb - Sbr);
 #pragma unroll
-    for (int i = 0; i < 6; ++i) {
-      P[i] = Saa * Jx[i] + Sab * Jy[i];
-      Q[i] = Sab * Jx[i] + Sbb * Jy[i];
-    }
-    int kq = 0;
+          for (int i = 0; i < 6; ++i) corr[i] = -(dA * Jx[i] + dB * Jy[i]);
+          corr[6] = invalid ? 0.0f : 1.0f;
+          if (le) {
+            const bool reset = sr0 < mn0;
+            mn0 = sr0;
 #pragma unroll
-    for (int i = 0; i < 6; ++i) {
+            for (int i = 0; i < 7; ++i) lds_ext[i][tid] = (reset ? 0.0f : lds_ext[i][tid]) + corr[i];
+          }
+          if (ge) {
+            const bool reset = sr0 > mx0;
+            mx0 = sr0;
 #pragma unroll
-      for (int j = i; j < 6; ++j) {
-        acc[kq] += P[i] * Jx[j] + Q[i] * Jy[j];
-        ++kq;
-      }
-    }
-#pragma unroll
-    for (int i = 0; i < 6; ++i) acc[21 + i] -= cA * Jx[i] + cB * Jy[i];
-    ninv += px.invalid ? 1.0f : 0.0f;
-
-    if (TRU) {
-      mn_all = fminf(mn_all, px.srmin);
-      mx_all = fmaxf(mx_all, px.srmax);
-      const bool le = px.sr0 <= mn0, ge = px.sr0 >= mx0;
-      if (le || ge) {
-        float corr[7];
-        const float dA = px.invalid ? 0.0f : (1e-6f * Sa - Sar);
-        const float dB = px.invalid ? 0.0f : (1e-6f * Sb - Sbr);
-#pragma unroll
-        for (int i = 0; i < 6; ++i) corr[i] = -(dA * Jx[i] + dB * Jy[i]);
-        corr[6] = px.invalid ? 0.0f : 1.0f;
-        if (le) {
-          const bool reset = px.sr0 < mn0;
-          mn0 = px.sr0;
-#pragma unroll
-          for (int i = 0; i < 7; ++i) lds_ext[i][tid] = (reset ? 0.0f : lds_ext[i][tid]) + corr[i];
-        }
-        if (ge) {
-          const bool reset = px.sr0 > mx0;
-          mx0 = px.sr0;
-#pragma unroll
-          for (int i = 0; i < 7; ++i) lds_ext[7 + i][tid] = (reset ? 0.0f : lds_ext[7 + i][tid]) + corr[i];
+            for (int i = 0; i < 7; ++i) lds_ext[7 + i][tid] = (reset ? 0.0f : lds_ext[7 + i][tid]) + corr[i];
+          }
         }
       }
     }
@@ -676,8 +679,8 @@ __global__ __launch_bounds__(kThreads) void ic_residual_kernel(IterParams p) {
   float mn_all = INFINITY, mn0 = INFINITY, lmn = 0.f, nmn = 0.f;
   float mx_all = -INFINITY, mx0 = -INFINITY, lmx = 0.f, nmx = 0.f;
   for (int step = 0; step < p.steps; ++step) {
-    const int y = (ty * p.steps + step) * kRowsPerStep + wave, x = tx * kTileW + lane;
-    if (x >= W || y >= H) continue;
+    const int y = (ty * p.steps + step) * kRowsPerStep + wave, x = tx * kTileOut + lane;
+    if (lane >= kTileOut || x >= W || y >= H) continue;
     const int pix = y * W + x;
     PixelFrame px;
     setup_pixel(p, b, x, y, p.invD0[(size_t)b * HW + pix], Rm, tv, fx, fy, cx, cy, px);
@@ -997,7 +1000,7 @@ struct Geometry {
 
 Geometry plan(const DpftLevelDesc& d) {
   Geometry g;
-  g.tiles_x = (d.W + kTileW - 1) / kTileW;
+  g.tiles_x = (d.W + kTileW - 3) / (kTileW - 2);  // 62 output columns per tile (2 halo lanes)
   const int row_groups = (d.H + kRowsPerStep - 1) / kRowsPerStep;
   int steps = kMaxSteps;
   // prefer >= 2048 workgroups (8 per CU) before taller tiles
