@@ -49,6 +49,12 @@
 
 #include "dpft_ic.h"
 
+// LLVM buffer-load intrinsics (declared at global scope: they bind by asm label).
+typedef int Rsrc __attribute__((ext_vector_type(4)));
+typedef float f32x2 __attribute__((ext_vector_type(2)));
+__device__ float llvm_buf_load_f32(Rsrc r, int voff, int soff, int aux) __asm("llvm.amdgcn.raw.buffer.load.f32");
+__device__ f32x2 llvm_buf_load_f32x2(Rsrc r, int voff, int soff, int aux) __asm("llvm.amdgcn.raw.buffer.load.v2f32");
+
 namespace {
 
 constexpr int kThreads = 256;          // 4 waves of 64
@@ -120,6 +126,8 @@ __device__ __forceinline__ int xcd_remap(int orig, int n) {
 
 struct Taps {
   int o00, o01, o10, o11;
+  int ob0, ob1;  // pair bases (row y0 / y1, column min(x0, W-2))
+  bool lo;       // x0 < W-1: the pair's first element is the (x0) tap
   float nw, ne, sw, se;
 };
 
@@ -144,6 +152,10 @@ __device__ __forceinline__ Taps make_taps(float u, float v, int H, int W) {
   t.o01 = y0 * W + x1;
   t.o10 = y1 * W + x0;
   t.o11 = y1 * W + x1;
+  const int xb = min(x0, W - 2);
+  t.ob0 = y0 * W + xb;
+  t.ob1 = y1 * W + xb;
+  t.lo = x0 == xb;
   t.nw = s * e;
   t.ne = s * w;
   t.sw = n * e;
@@ -315,24 +327,38 @@ __device__ __forceinline__ void ext_wave_reduce(Extremum& e) {
 // ---------------------------------------------------------------- buffer loads
 // Raw buffer loads: a scalar resource per tensor plane-set, a per-lane byte
 // offset that is fixed per pixel (or per tile column) and a scalar offset per
-// channel / row -- no vector ALU spent on addresses, and any offset past the
-// plane set reads 0 instead of faulting.
-__device__ __forceinline__ __amdgpu_buffer_rsrc_t rsrc(const void* p, uint32_t bytes) {
-  return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(p), (short)0, (int)bytes, 0x00020000);
+// channel / row -- no vector ALU spent on addresses, and an offset past the
+// plane set reads 0 instead of faulting.  (The LLVM intrinsics are used
+// directly: ROCm 7.2's __builtin_amdgcn_raw_buffer_load_b64 drops the second
+// dword on gfx950.)
+
+__device__ __forceinline__ Rsrc rsrc(const void* p, uint32_t bytes) {
+  const unsigned long long a = (unsigned long long)p;
+  Rsrc r;
+  r.x = (int)(uint32_t)a;
+  r.y = (int)(uint32_t)(a >> 32);  // stride 0
+  r.z = (int)bytes;
+  r.w = 0x00020000;
+  return r;
 }
-__device__ __forceinline__ float bld(__amdgpu_buffer_rsrc_t r, int voff, int soff) {
-  return __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(r, voff, soff, 0));
-}
+__device__ __forceinline__ float bld(Rsrc r, int voff, int soff) { return llvm_buf_load_f32(r, voff, soff, 0); }
+__device__ __forceinline__ f32x2 bld2(Rsrc r, int voff, int soff) { return llvm_buf_load_f32x2(r, voff, soff, 0); }
 
 struct Gather4 {
   float a, b, c, d;
 };
-__device__ __forceinline__ Gather4 gather4(__amdgpu_buffer_rsrc_t r, const Taps& t, int soff) {
+// The two taps of a sampling row are adjacent columns: one 8-byte load each.
+// The pair starts at min(x0, W-2) so it never leaves the row; at x0 = W-1 the
+// clamped neighbour x1 = x0 is the pair's second element, exactly like the
+// reference's border clamp.
+__device__ __forceinline__ Gather4 gather4(Rsrc r, const Taps& t, int soff) {
+  const f32x2 p0 = bld2(r, t.ob0 * 4, soff);
+  const f32x2 p1 = bld2(r, t.ob1 * 4, soff);
   Gather4 g;
-  g.a = bld(r, t.o00 * 4, soff);
-  g.b = bld(r, t.o01 * 4, soff);
-  g.c = bld(r, t.o10 * 4, soff);
-  g.d = bld(r, t.o11 * 4, soff);
+  g.a = t.lo ? p0.x : p0.y;
+  g.b = p0.y;
+  g.c = t.lo ? p1.x : p1.y;
+  g.d = p1.y;
   return g;
 }
 
@@ -359,7 +385,7 @@ __device__ __forceinline__ void sobel_cols(float top, float mid, float bot, floa
   const float D = bot - top;
   const float x = lane_from_right(V) - lane_from_left(V);
   const float y = (lane_from_left(D) + 2.0f * D) + lane_from_right(D);
-  const float inv = rsqrtf(x * x + y * y + 1e-8f);
+  const float inv = __builtin_amdgcn_rsqf(x * x + y * y + 1e-8f);  // argument >= 1e-8: no denormal path
   gx = x * inv;
   gy = y * inv;
 }
@@ -511,15 +537,16 @@ __global__ __launch_bounds__(kThreads, DPFT_MIN_WAVES) void ic_reduce_kernel(Ite
         const float r = frv - f0v;
         const float rw = r * is_c;
         const float rk = r * kk_c;
-        const float a = -(gx * is_c + rk * hx_c);
-        const float bq = -(gy * is_c + rk * hy_c);
-        Saa += a * a;
-        Sab += a * bq;
-        Sbb += bq * bq;
-        Sa += a;
-        Sb += bq;
-        Sar += a * rw;
-        Sbr += bq * rw;
+        // na = -a, nb = -b (a, b of algorithms.py:872); the linear sums are negated after the loop
+        const float na = gx * is_c + rk * hx_c;
+        const float nb = gy * is_c + rk * hy_c;
+        Saa += na * na;
+        Sab += na * nb;
+        Sbb += nb * nb;
+        Sa += na;
+        Sb += nb;
+        Sar += na * rw;
+        Sbr += nb * rw;
       }
     };
 
@@ -528,6 +555,10 @@ __global__ __launch_bounds__(kThreads, DPFT_MIN_WAVES) void ic_reduce_kernel(Ite
       unit(2 * kp, LE, LO);
       unit(2 * kp + 1, LO, LE);
     }
+    Sa = -Sa;
+    Sb = -Sb;
+    Sar = -Sar;
+    Sbr = -Sbr;
 
     if (out_lane) {
       float Jx[6], Jy[6];
