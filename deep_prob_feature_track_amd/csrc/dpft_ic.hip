@@ -2,7 +2,7 @@
 // inverse-compositional (U_IC) solver of Deep Probabilistic Feature-metric
 // Tracking.  ABI and semantics: include/dpft_ic.h.
 //
-// One Gauss-Newton iteration at one pyramid level is two launches:
+// One Gauss-Newton iteration at one pyramid level is ONE launch:
 //
 //   ic_reduce_kernel   fused, HBM-bound pass over every pixel of every pair:
 //                      inverse-depth warp (geometry.py:291-323), bilinear
@@ -10,16 +10,19 @@
 //                      occlusion + object masks (geometry.py:334-350,
 //                      algorithms.py:1999-2008), uncertainty-weighted residual
 //                      (algorithms.py:1960-1989), Sobel gradients of f0 and
-//                      sigma0 recomputed from an LDS tile (algorithms.py:
-//                      1844-1865, never stored), the per-channel inverse
-//                      Jacobian (algorithms.py:867-887, 1867-1917) folded into
-//                      channel sums, and the 21 + 6 normal-equation partials
-//                      (algorithms.py:812-834).  Each workgroup writes one
-//                      fixed-size record: no atomics, deterministic.
-//   ic_finalize_kernel one workgroup per pair: fixed-order fp64 reduction of
-//                      that pair's records, the batch-global truncated-sigma
-//                      correction, Levenberg damping, fp64 6x6 solve and the
-//                      SE(3) update (algorithms.py:2017-2103), in place.
+//                      sigma0 recomputed in registers with DPP lane shifts
+//                      (algorithms.py:1844-1865, never stored), the per-channel
+//                      inverse Jacobian (algorithms.py:867-887, 1867-1917)
+//                      folded into channel sums, and the 21 + 6 normal-equation
+//                      partials (algorithms.py:812-834).  Each workgroup writes
+//                      one fixed-size record: no atomics on data, deterministic.
+//                      The LAST workgroup to finish (threadfence handshake) then
+//                      reduces every pair's records in a fixed order in fp64,
+//                      applies the batch-global truncated-sigma correction,
+//                      Levenberg damping, the 6x6 solve and the SE(3) update
+//                      (algorithms.py:2017-2103), in place.
+//
+// plus, on the first iteration of a level, minmax_kernel (sigma0 extrema).
 //
 // J is never materialised: per pixel and channel the reference's J_c is
 // -(a_c Jx + b_c Jy), so sum_c J_c J_c^T = Saa JxJx^T + Sab (JxJy^T + JyJx^T)
@@ -90,8 +93,22 @@ constexpr int R_NMX = 45;
 constexpr int L_SUM = 0, L_NINV = 1, L_MN_ALL = 2, L_MN0 = 3, L_LMN = 4, L_NMN = 5,
               L_MX_ALL = 6, L_MX0 = 7, L_LMX = 8, L_NMX = 9;
 
-// workspace: [ctrl 256 B][records]
-constexpr size_t kCtrlBytes = 256;
+// workspace: [ctrl 8 KiB][records].  ctrl words: sigma0 extrema (order-encoded),
+// the two "blocks done" counters of the last-block finalizers, and the per-block
+// partial extrema of the sigma0 pass.  The counters are zero between calls: the
+// caller zero-fills the workspace once, every last block resets its counter.
+constexpr int kCtlMin = 0, kCtlMax = 1, kCtlDone = 2, kCtlMMDone = 3, kCtlResDone = 4, kCtlPart = 64, kCtlPair = 1152;
+constexpr int kMaxMMBlocks = 512;
+constexpr int kMaxPairs = 2048;  // per call (one completion counter per pair)
+constexpr size_t kCtrlBytes = 16384;
+static_assert((kCtlPart + 2 * kMaxMMBlocks) * 4 <= kCtlPair * 4, "ctrl area");
+static_assert((kCtlPair + kMaxPairs) * 4 <= kCtrlBytes, "ctrl area");
+// per-pair record (fp64) written by the last workgroup of each pair
+constexpr int P_S = 0;        // 28: JtJ upper (21), JtR (6), #invalid
+constexpr int P_CMN = 28;     // 7: JtR / count corrections of the blocks at the pair's min sigma_r ch0
+constexpr int P_CMX = 35;     // 7: same at the max
+constexpr int P_MN_ALL = 42, P_MN0 = 43, P_MX_ALL = 44, P_MX0 = 45;
+constexpr int kPRec = 48;
 
 thread_local char g_err[512] = "";
 
@@ -111,6 +128,38 @@ __device__ __forceinline__ uint32_t enc_ord(float f) {
 __device__ __forceinline__ float dec_ord(uint32_t e) {
   uint32_t u = (e & 0x80000000u) ? (e & 0x7fffffffu) : ~e;
   return __uint_as_float(u);
+}
+
+// Threadfence-reduction handshake: every workgroup publishes its record, then
+// the one that arrives last (counter == total-1) sees all records and finalizes.
+// Agent-scope fences make the records of workgroups on other XCDs visible.
+// Records cross workgroups (and XCDs, whose L2s are not coherent with each
+// other) only through agent-scope relaxed atomic stores / loads (sc1: coherent
+// at the device level), so the handshake needs no agent-scope fence -- whose
+// L2 write-back / invalidate per workgroup would wreck the streaming reuse.
+// Each wave waits for its record stores to be acknowledged before the barrier;
+// only then does thread 0 bump the counter.
+template <class T>
+__device__ __forceinline__ void st_ag(T* p, T v) {
+  __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+template <class T>
+__device__ __forceinline__ T ld_ag(const T* p) {
+  return __hip_atomic_load(const_cast<T*>(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+__device__ bool block_is_last(uint32_t* counter, uint32_t total) {
+  __shared__ int s_last;
+  __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0): this wave's stores are complete
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    const uint32_t prev = __hip_atomic_fetch_add(counter, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const int last = prev == total - 1u;
+    if (last) st_ag(counter, 0u);  // ready for the next launch
+    s_last = last;
+  }
+  __syncthreads();
+  return s_last != 0;
 }
 
 __device__ __forceinline__ int wave_id() { return __builtin_amdgcn_readfirstlane(threadIdx.x >> 6); }
@@ -202,6 +251,23 @@ __device__ __forceinline__ Warp warp_point(int x, int y, float d, const float* _
   return w;
 }
 
+// Last-block finalize parameters (one record per workgroup, fixed-order fp64 sums).
+struct FinParams {
+  const float* rec;
+  double* prec;       // [B][kPRec] per-pair records
+  uint32_t* pair_cnt; // [B] completion counters
+  uint32_t* done_cnt; // pairs finished
+  int nblocks, per_pair, HW;
+  uint32_t flags;
+  float* R;
+  float* t;
+  float* jtj_out;
+  float* jtr_out;
+  int32_t* invalid_out;
+  float* loss_out;
+  uint32_t* status;
+};
+
 struct IterParams {
   const float* f0;
   const float* f1;
@@ -217,8 +283,10 @@ struct IterParams {
   int B, C, Cs, H, W;
   int tiles_x, tiles_y, steps, nblocks;
   uint32_t flags;
-  const uint32_t* ctrl;  // [0]=enc min sigma0, [1]=enc max sigma0
+  uint32_t* ctrl;  // see kCtl*
   float* rec;
+  int fin_on;      // 0: records only (timing hook); 1: last workgroup finalizes
+  FinParams fin;
 };
 
 // Per-pixel state that lives across the channel loop of one step.
@@ -394,6 +462,300 @@ struct ChanLoads {
   float t, m, b;  // f0 column in rows y-1, y, y+1
   Gather4 g;      // f1 taps
 };
+
+// ============================================================ last-block finalize
+__device__ __forceinline__ double wave_sum_d(double v) {
+  for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off);
+  return v;
+}
+
+// Global (whole-batch) extrema of sigma_r over every record (all threads call).
+__device__ void global_extrema(const float* rec, int nblocks, int imn, int imx, float& gmin, float& gmax) {
+  __shared__ float sm[2][4];
+  float mn = INFINITY, mx = -INFINITY;
+  for (int k = threadIdx.x; k < nblocks; k += kThreads) {
+    mn = fminf(mn, ld_ag(rec + (size_t)k * kRec + imn));
+    mx = fmaxf(mx, ld_ag(rec + (size_t)k * kRec + imx));
+  }
+  for (int off = 32; off > 0; off >>= 1) {
+    mn = fminf(mn, __shfl_xor(mn, off));
+    mx = fmaxf(mx, __shfl_xor(mx, off));
+  }
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  if (lane == 0) {
+    sm[0][wave] = mn;
+    sm[1][wave] = mx;
+  }
+  __syncthreads();
+  gmin = fminf(fminf(sm[0][0], sm[0][1]), fminf(sm[0][2], sm[0][3]));
+  gmax = fmaxf(fmaxf(sm[1][0], sm[1][1]), fmaxf(sm[1][2], sm[1][3]));
+}
+
+// Solve (JtJ + 1e-6 tr(JtJ) I) xi = JtR in fp64 (algorithms.py:2094-2103: the
+// damped matrix is SPD, so a fully unrolled register Cholesky replaces the
+// reference's batched inverse) and apply the inverse-compositional update
+// (algorithms.py:2035-2054, geometry.py:105-123, 163-185):
+// R <- R Exp(-w), t <- R (-Exp(-w) v) + t.
+__device__ void solve_and_update(const double* jtj_u, const double* jtr, float* Rp, float* tp) {
+  double A[6][6];
+  int k = 0;
+#pragma unroll
+  for (int i = 0; i < 6; ++i)
+#pragma unroll
+    for (int j = i; j < 6; ++j) {
+      A[i][j] = jtj_u[k];
+      A[j][i] = jtj_u[k];
+      ++k;
+    }
+  const double tr = ((((A[0][0] + A[1][1]) + A[2][2]) + A[3][3]) + A[4][4]) + A[5][5];
+#pragma unroll
+  for (int i = 0; i < 6; ++i) A[i][i] += 1e-6 * tr;
+  double L[6][6], invd[6];
+#pragma unroll
+  for (int j = 0; j < 6; ++j) {
+    double dj = A[j][j];
+#pragma unroll
+    for (int m = 0; m < j; ++m) dj -= L[j][m] * L[j][m];
+    const double ljj = sqrt(dj);
+    invd[j] = 1.0 / ljj;
+#pragma unroll
+    for (int i = j + 1; i < 6; ++i) {
+      double v = A[i][j];
+#pragma unroll
+      for (int m = 0; m < j; ++m) v -= L[i][m] * L[j][m];
+      L[i][j] = v * invd[j];
+    }
+  }
+  double z[6], xi[6];
+#pragma unroll
+  for (int i = 0; i < 6; ++i) {
+    double v = jtr[i];
+#pragma unroll
+    for (int m = 0; m < i; ++m) v -= L[i][m] * z[m];
+    z[i] = v * invd[i];
+  }
+#pragma unroll
+  for (int i = 5; i >= 0; --i) {
+    double v = z[i];
+#pragma unroll
+    for (int m = i + 1; m < 6; ++m) v -= L[m][i] * xi[m];
+    xi[i] = v * invd[i];
+  }
+  // dR = Exp(-w): Rodrigues, NaN at |w| = 0 exactly as the reference.
+  const double w0 = -xi[0], w1 = -xi[1], w2 = -xi[2];
+  const double th = sqrt(w0 * w0 + w1 * w1 + w2 * w2);
+  const double k0 = w0 / th, k1 = w1 / th, k2 = w2 / th;
+  const double Kx[9] = {0.0, -k2, k1, k2, 0.0, -k0, -k1, k0, 0.0};
+  double sn, cs;
+  sincos(th, &sn, &cs);
+  const double cs1 = 1.0 - cs;
+  double dR[9];
+#pragma unroll
+  for (int i = 0; i < 3; ++i)
+#pragma unroll
+    for (int j = 0; j < 3; ++j) {
+      const double kk = Kx[3 * i] * Kx[j] + Kx[3 * i + 1] * Kx[3 + j] + Kx[3 * i + 2] * Kx[6 + j];
+      dR[3 * i + j] = ((i == j) ? 1.0 : 0.0) + Kx[3 * i + j] * sn + kk * cs1;
+    }
+  double dt[3];
+#pragma unroll
+  for (int i = 0; i < 3; ++i) dt[i] = -(dR[3 * i] * xi[3] + dR[3 * i + 1] * xi[4] + dR[3 * i + 2] * xi[5]);
+  double R0[9], t0[3];
+#pragma unroll
+  for (int i = 0; i < 9; ++i) R0[i] = Rp[i];
+#pragma unroll
+  for (int i = 0; i < 3; ++i) t0[i] = tp[i];
+#pragma unroll
+  for (int i = 0; i < 3; ++i) {
+#pragma unroll
+    for (int j = 0; j < 3; ++j)
+      Rp[3 * i + j] = (float)(R0[3 * i] * dR[j] + R0[3 * i + 1] * dR[3 + j] + R0[3 * i + 2] * dR[6 + j]);
+    tp[i] = (float)(R0[3 * i] * dt[0] + R0[3 * i + 1] * dt[1] + R0[3 * i + 2] * dt[2] + t0[i]);
+  }
+}
+
+// Workgroup-wide min / max of two floats (all threads call; result in all threads).
+__device__ void block_minmax2(float& mn_a, float& mx_a, float& mn_b, float& mx_b) {
+  __shared__ float sm[4][4];
+  for (int off = 32; off > 0; off >>= 1) {
+    mn_a = fminf(mn_a, __shfl_xor(mn_a, off));
+    mx_a = fmaxf(mx_a, __shfl_xor(mx_a, off));
+    mn_b = fminf(mn_b, __shfl_xor(mn_b, off));
+    mx_b = fmaxf(mx_b, __shfl_xor(mx_b, off));
+  }
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  __syncthreads();  // sm may still be read by a previous call
+  if (lane == 0) {
+    sm[0][wave] = mn_a;
+    sm[1][wave] = mx_a;
+    sm[2][wave] = mn_b;
+    sm[3][wave] = mx_b;
+  }
+  __syncthreads();
+  mn_a = fminf(fminf(sm[0][0], sm[0][1]), fminf(sm[0][2], sm[0][3]));
+  mx_a = fmaxf(fmaxf(sm[1][0], sm[1][1]), fmaxf(sm[1][2], sm[1][3]));
+  mn_b = fminf(fminf(sm[2][0], sm[2][1]), fminf(sm[2][2], sm[2][3]));
+  mx_b = fmaxf(fmaxf(sm[3][0], sm[3][1]), fmaxf(sm[3][2], sm[3][3]));
+}
+
+// Run by the last workgroup of pair b: reduce its per-workgroup records into one
+// fp64 pair record.  Thread (j, i) sums component i over records j, j+8, ...
+// (4 loads in flight), the 8 partials are then added in a fixed order.  The
+// truncated-sigma corrections of the workgroups that attain the pair's extremum
+// of sigma_r (channel 0) are kept apart: whether they apply depends on the
+// batch-global extremum, known only when every pair is done.
+__device__ void pair_reduce(const FinParams& q, int b) {
+  __shared__ double part[8][32], pmn[8][8], pmx[8][8];
+  const int tid = threadIdx.x, i = tid & 31, j = tid >> 5;
+  const bool tru = (q.flags & DPFT_REMOVE_TRU_SIGMA) != 0;
+  const float* rec = q.rec + (size_t)b * q.per_pair * kRec;
+  const int n = q.per_pair;
+  float mn_all = INFINITY, mx_all = -INFINITY, mn0 = INFINITY, mx0 = -INFINITY;
+  if (tru) {
+    float a = INFINITY, c = -INFINITY;
+    for (int k = tid; k < n; k += kThreads) {
+      const float* r = rec + (size_t)k * kRec;
+      mn_all = fminf(mn_all, ld_ag(r + R_MN_ALL));
+      mx_all = fmaxf(mx_all, ld_ag(r + R_MX_ALL));
+      a = fminf(a, ld_ag(r + R_MN0));
+      c = fmaxf(c, ld_ag(r + R_MX0));
+    }
+    mn0 = a;
+    mx0 = c;
+    block_minmax2(mn_all, mx_all, mn0, mx0);
+  }
+  const int ci = i - 21;  // correction slot (0..6) of components 21..27
+  double acc = 0.0, cmn = 0.0, cmx = 0.0;
+  if (i < 28) {
+    for (int k0 = j; k0 < n; k0 += 32) {
+      float v[4], m[4], x[4], cn[4], cx[4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const int k = k0 + 8 * u;
+        const float* r = rec + (size_t)min(k, n - 1) * kRec;
+        const bool ok = k < n;
+        v[u] = ok ? ld_ag(r + i) : 0.0f;
+        if (tru && i >= 21) {
+          m[u] = ok ? ld_ag(r + R_MN0) : NAN;
+          x[u] = ok ? ld_ag(r + R_MX0) : NAN;
+          cn[u] = ld_ag(r + R_CMN + ci);  // R_CMN + 6 == R_NMN
+          cx[u] = ld_ag(r + R_CMX + ci);  // R_CMX + 6 == R_NMX
+        }
+      }
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        acc += (double)v[u];
+        if (tru && i >= 21) {
+          if (m[u] == mn0) cmn += (double)cn[u];
+          if (x[u] == mx0) cmx += (double)cx[u];
+        }
+      }
+    }
+  }
+  part[j][i] = acc;
+  if (i >= 21 && i < 28) {
+    pmn[j][ci] = cmn;
+    pmx[j][ci] = cmx;
+  }
+  __syncthreads();
+  double* pr = q.prec + (size_t)b * kPRec;
+  if (tid < 28) {
+    double v = part[0][tid];
+#pragma unroll
+    for (int m = 1; m < 8; ++m) v += part[m][tid];
+    st_ag(pr + P_S + tid, (double)(v));
+  } else if (tid >= 32 && tid < 39) {
+    double v = pmn[0][tid - 32];
+#pragma unroll
+    for (int m = 1; m < 8; ++m) v += pmn[m][tid - 32];
+    st_ag(pr + P_CMN + tid - 32, (double)(v));
+  } else if (tid >= 64 && tid < 71) {
+    double v = pmx[0][tid - 64];
+#pragma unroll
+    for (int m = 1; m < 8; ++m) v += pmx[m][tid - 64];
+    st_ag(pr + P_CMX + tid - 64, (double)(v));
+  } else if (tid == 96) {
+    st_ag(pr + P_MN_ALL, (double)(mn_all));
+    st_ag(pr + P_MN0, (double)(mn0));
+    st_ag(pr + P_MX_ALL, (double)(mx_all));
+    st_ag(pr + P_MX0, (double)(mx0));
+  }
+}
+
+// Run by the workgroup that completes the last pair: batch-global truncated-sigma
+// extrema over the pair records, corrections, then one thread per pair solves and
+// updates its pose (algorithms.py:2017-2103).
+__device__ void finalize_batch(const FinParams& q) {
+  const bool tru = (q.flags & DPFT_REMOVE_TRU_SIGMA) != 0;
+  const int B = q.nblocks / q.per_pair;
+  float gmin = INFINITY, gmax = -INFINITY, u0 = INFINITY, u1 = -INFINITY;
+  if (tru) {
+    for (int b = threadIdx.x; b < B; b += kThreads) {
+      gmin = fminf(gmin, (float)ld_ag(q.prec + (size_t)b * kPRec + P_MN_ALL));
+      gmax = fmaxf(gmax, (float)ld_ag(q.prec + (size_t)b * kPRec + P_MX_ALL));
+    }
+    block_minmax2(gmin, gmax, u0, u1);
+  }
+  for (int b = threadIdx.x; b < B; b += kThreads) {
+    const double* pr = q.prec + (size_t)b * kPRec;
+    double sv[28];
+#pragma unroll
+    for (int k = 0; k < 28; ++k) sv[k] = ld_ag(pr + P_S + k);
+    if (tru) {
+      if ((float)ld_ag(pr + P_MN0) == gmin)
+#pragma unroll
+        for (int k = 0; k < 7; ++k) sv[21 + k] += ld_ag(pr + P_CMN + k);
+      if (gmax != gmin && (float)ld_ag(pr + P_MX0) == gmax)
+#pragma unroll
+        for (int k = 0; k < 7; ++k) sv[21 + k] += ld_ag(pr + P_CMX + k);
+    }
+    bool finite = true;
+#pragma unroll
+    for (int k = 0; k < 27; ++k) finite = finite && isfinite(sv[k]);
+    if (!finite && q.status) atomicOr(q.status, DPFT_STATUS_NONFINITE);
+    if (q.jtj_out) {
+      int k = 0;
+#pragma unroll
+      for (int r = 0; r < 6; ++r)
+#pragma unroll
+        for (int c = r; c < 6; ++c) {
+          q.jtj_out[36 * b + 6 * r + c] = (float)sv[k];
+          q.jtj_out[36 * b + 6 * c + r] = (float)sv[k];
+          ++k;
+        }
+    }
+    if (q.jtr_out)
+#pragma unroll
+      for (int k = 0; k < 6; ++k) q.jtr_out[6 * b + k] = (float)sv[21 + k];
+    if (q.invalid_out) q.invalid_out[b] = (int32_t)sv[27];
+    solve_and_update(sv, sv + 21, q.R + 9 * b, q.t + 3 * b);
+  }
+}
+
+// Last workgroup of a residual launch: loss[b] = sum / (HW - #invalid)
+// (algorithms.py:2119-2137).
+__device__ void finalize_loss(const FinParams& q) {
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const bool tru = (q.flags & DPFT_REMOVE_TRU_SIGMA) != 0;
+  float gmin = 0.f, gmax = 0.f;
+  if (tru) global_extrema(q.rec, q.nblocks, L_MN_ALL, L_MX_ALL, gmin, gmax);
+  const int B = q.nblocks / q.per_pair;
+  for (int b = wave; b < B; b += 4) {
+    double sum = 0.0, ninv = 0.0;
+    for (int k = lane; k < q.per_pair; k += 64) {
+      const float* r = q.rec + (size_t)(b * q.per_pair + k) * kRec;
+      sum += ld_ag(r + L_SUM);
+      ninv += ld_ag(r + L_NINV);
+      if (tru) {
+        if (ld_ag(r + L_MN0) == gmin) { sum -= ld_ag(r + L_LMN); ninv += ld_ag(r + L_NMN); }
+        if (gmax != gmin && ld_ag(r + L_MX0) == gmax) { sum -= ld_ag(r + L_LMX); ninv += ld_ag(r + L_NMX); }
+      }
+    }
+    sum = wave_sum_d(sum);
+    ninv = wave_sum_d(ninv);
+    if (lane == 0) q.loss_out[b] = (float)(sum / ((double)q.HW - ninv));
+  }
+}
 
 // ============================================================ fused reduce kernel
 // Loads of channel chunk k+1 are issued before chunk k's math; chunks go in
@@ -658,7 +1020,7 @@ __global__ __launch_bounds__(kThreads, DPFT_MIN_WAVES) void ic_reduce_kernel(Ite
   __syncthreads();
   float* out = p.rec + (size_t)bid * kRec;
   if (tid < 28) {
-    out[tid] = ((red[0][tid] + red[1][tid]) + red[2][tid]) + red[3][tid];
+    st_ag(out + tid, (float)(((red[0][tid] + red[1][tid]) + red[2][tid]) + red[3][tid]));
   } else if (TRU && tid == 64) {
     Extremum e;
     e.all = red[0][R_MN_ALL];
@@ -666,10 +1028,10 @@ __global__ __launch_bounds__(kThreads, DPFT_MIN_WAVES) void ic_reduce_kernel(Ite
     e.n = red[0][R_NMN];
     for (int k = 0; k < 6; ++k) e.c[k] = red[0][R_CMN + k];
     for (int w = 1; w < 4; ++w) ext_merge<true>(e, red[w][R_MN_ALL], red[w][R_MN0], &red[w][R_CMN], red[w][R_NMN]);
-    out[R_MN_ALL] = e.all;
-    out[R_MN0] = e.v0;
-    out[R_NMN] = e.n;
-    for (int k = 0; k < 6; ++k) out[R_CMN + k] = e.c[k];
+    st_ag(out + R_MN_ALL, (float)(e.all));
+    st_ag(out + R_MN0, (float)(e.v0));
+    st_ag(out + R_NMN, (float)(e.n));
+    for (int k = 0; k < 6; ++k) st_ag(out + R_CMN + k, (float)(e.c[k]));
   } else if (TRU && tid == 128) {
     Extremum e;
     e.all = red[0][R_MX_ALL];
@@ -677,10 +1039,14 @@ __global__ __launch_bounds__(kThreads, DPFT_MIN_WAVES) void ic_reduce_kernel(Ite
     e.n = red[0][R_NMX];
     for (int k = 0; k < 6; ++k) e.c[k] = red[0][R_CMX + k];
     for (int w = 1; w < 4; ++w) ext_merge<false>(e, red[w][R_MX_ALL], red[w][R_MX0], &red[w][R_CMX], red[w][R_NMX]);
-    out[R_MX_ALL] = e.all;
-    out[R_MX0] = e.v0;
-    out[R_NMX] = e.n;
-    for (int k = 0; k < 6; ++k) out[R_CMX + k] = e.c[k];
+    st_ag(out + R_MX_ALL, (float)(e.all));
+    st_ag(out + R_MX0, (float)(e.v0));
+    st_ag(out + R_NMX, (float)(e.n));
+    for (int k = 0; k < 6; ++k) st_ag(out + R_CMX + k, (float)(e.c[k]));
+  }
+  if (p.fin_on && block_is_last(p.fin.pair_cnt + b, (uint32_t)(p.tiles_x * p.tiles_y))) {
+    pair_reduce(p.fin, b);
+    if (block_is_last(p.fin.done_cnt, (uint32_t)p.B)) finalize_batch(p.fin);
   }
 }
 
@@ -775,10 +1141,11 @@ __global__ __launch_bounds__(kThreads) void ic_residual_kernel(IterParams p) {
       if (red[w][L_MX0] > x0v) { x0v = red[w][L_MX0]; lx = red[w][L_LMX]; nx = red[w][L_NMX]; }
       else if (red[w][L_MX0] == x0v) { lx += red[w][L_LMX]; nx += red[w][L_NMX]; }
     }
-    out[L_SUM] = s; out[L_NINV] = ni;
-    out[L_MN_ALL] = ma; out[L_MN0] = m0; out[L_LMN] = lm; out[L_NMN] = nm;
-    out[L_MX_ALL] = xa; out[L_MX0] = x0v; out[L_LMX] = lx; out[L_NMX] = nx;
+    st_ag(out + L_SUM, (float)(s)); st_ag(out + L_NINV, (float)(ni));
+    st_ag(out + L_MN_ALL, (float)(ma)); st_ag(out + L_MN0, (float)(m0)); st_ag(out + L_LMN, (float)(lm)); st_ag(out + L_NMN, (float)(nm));
+    st_ag(out + L_MX_ALL, (float)(xa)); st_ag(out + L_MX0, (float)(x0v)); st_ag(out + L_LMX, (float)(lx)); st_ag(out + L_NMX, (float)(nx));
   }
+  if (block_is_last(p.ctrl + kCtlResDone, (uint32_t)p.nblocks)) finalize_loss(p.fin);
 }
 
 
@@ -806,207 +1173,10 @@ __global__ __launch_bounds__(kThreads) void ic_debug_pixels_kernel(IterParams p,
   o[4 * HW] = px.invalid ? 1.0f : 0.0f;
 }
 
-// ============================================================ finalize
-struct FinParams {
-  const float* rec;
-  int nblocks, per_pair, HW;
-  uint32_t flags;
-  float* R;
-  float* t;
-  float* jtj_out;
-  float* jtr_out;
-  int32_t* invalid_out;
-  float* loss_out;
-  uint32_t* status;
-};
-
-__device__ __forceinline__ double wave_sum_d(double v) {
-  for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off);
-  return v;
-}
-
-// Global (whole-batch) extrema of sigma_r from every record.
-__device__ void global_extrema(const float* rec, int nblocks, int imn, int imx, float& gmin, float& gmax) {
-  __shared__ float sm[2][4];
-  float mn = INFINITY, mx = -INFINITY;
-  for (int k = threadIdx.x; k < nblocks; k += kThreads) {
-    mn = fminf(mn, rec[(size_t)k * kRec + imn]);
-    mx = fmaxf(mx, rec[(size_t)k * kRec + imx]);
-  }
-  for (int off = 32; off > 0; off >>= 1) {
-    mn = fminf(mn, __shfl_xor(mn, off));
-    mx = fmaxf(mx, __shfl_xor(mx, off));
-  }
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  if (lane == 0) {
-    sm[0][wave] = mn;
-    sm[1][wave] = mx;
-  }
-  __syncthreads();
-  gmin = fminf(fminf(sm[0][0], sm[0][1]), fminf(sm[0][2], sm[0][3]));
-  gmax = fmaxf(fmaxf(sm[1][0], sm[1][1]), fmaxf(sm[1][2], sm[1][3]));
-}
-
-// Solve (JtJ + 1e-6 tr(JtJ) I) xi = JtR in fp64 with partial pivoting and apply
-// the inverse-compositional update (algorithms.py:2035-2054, geometry.py:105-123,
-// 163-185): R <- R Exp(-w), t <- R (-Exp(-w) v) + t.
-__device__ void solve_and_update(const double* jtj_u, const double* jtr, float* Rp, float* tp) {
-  double A[6][7];
-  int k = 0;
-  for (int i = 0; i < 6; ++i)
-    for (int j = i; j < 6; ++j) {
-      A[i][j] = jtj_u[k];
-      A[j][i] = jtj_u[k];
-      ++k;
-    }
-  double tr = 0.0;
-  for (int i = 0; i < 6; ++i) tr += A[i][i];
-  for (int i = 0; i < 6; ++i) {
-    A[i][i] += 1e-6 * tr;
-    A[i][6] = jtr[i];
-  }
-  for (int c = 0; c < 6; ++c) {
-    int piv = c;
-    for (int r = c + 1; r < 6; ++r)
-      if (fabs(A[r][c]) > fabs(A[piv][c])) piv = r;
-    if (piv != c)
-      for (int j = 0; j < 7; ++j) {
-        const double tmp = A[c][j];
-        A[c][j] = A[piv][j];
-        A[piv][j] = tmp;
-      }
-    const double inv = 1.0 / A[c][c];
-    for (int r = c + 1; r < 6; ++r) {
-      const double f = A[r][c] * inv;
-      for (int j = c; j < 7; ++j) A[r][j] -= f * A[c][j];
-    }
-  }
-  double xi[6];
-  for (int i = 5; i >= 0; --i) {
-    double s = A[i][6];
-    for (int j = i + 1; j < 6; ++j) s -= A[i][j] * xi[j];
-    xi[i] = s / A[i][i];
-  }
-  // dR = Exp(-w): Rodrigues, NaN at |w| = 0 exactly as the reference.
-  const double w0 = -xi[0], w1 = -xi[1], w2 = -xi[2];
-  const double th = sqrt(w0 * w0 + w1 * w1 + w2 * w2);
-  const double k0 = w0 / th, k1 = w1 / th, k2 = w2 / th;
-  const double Kx[9] = {0.0, -k2, k1, k2, 0.0, -k0, -k1, k0, 0.0};
-  double KK[9];
-  for (int i = 0; i < 3; ++i)
-    for (int j = 0; j < 3; ++j) {
-      double s = 0.0;
-      for (int m = 0; m < 3; ++m) s += Kx[3 * i + m] * Kx[3 * m + j];
-      KK[3 * i + j] = s;
-    }
-  const double sn = sin(th), cs1 = 1.0 - cos(th);
-  double dR[9];
-  for (int i = 0; i < 9; ++i) dR[i] = ((i % 4 == 0) ? 1.0 : 0.0) + Kx[i] * sn + KK[i] * cs1;
-  double dt[3];
-  for (int i = 0; i < 3; ++i) dt[i] = -(dR[3 * i] * xi[3] + dR[3 * i + 1] * xi[4] + dR[3 * i + 2] * xi[5]);
-  double R0[9], t0[3];
-  for (int i = 0; i < 9; ++i) R0[i] = Rp[i];
-  for (int i = 0; i < 3; ++i) t0[i] = tp[i];
-  for (int i = 0; i < 3; ++i) {
-    for (int j = 0; j < 3; ++j) {
-      double s = 0.0;
-      for (int m = 0; m < 3; ++m) s += R0[3 * i + m] * dR[3 * m + j];
-      Rp[3 * i + j] = (float)s;
-    }
-    tp[i] = (float)(R0[3 * i] * dt[0] + R0[3 * i + 1] * dt[1] + R0[3 * i + 2] * dt[2] + t0[i]);
-  }
-}
-
-__global__ __launch_bounds__(kThreads) void ic_finalize_kernel(FinParams q) {
-  const int b = blockIdx.x;
-  const bool tru = (q.flags & DPFT_REMOVE_TRU_SIGMA) != 0;
-  float gmin = 0.f, gmax = 0.f;
-  if (tru) global_extrema(q.rec, q.nblocks, R_MN_ALL, R_MX_ALL, gmin, gmax);
-
-  double s[28];
-  for (int k = 0; k < 28; ++k) s[k] = 0.0;
-  const int first = b * q.per_pair;
-  for (int k = threadIdx.x; k < q.per_pair; k += kThreads) {
-    const float* r = q.rec + (size_t)(first + k) * kRec;
-    for (int i = 0; i < 28; ++i) s[i] += (double)r[i];
-    if (tru) {
-      if (r[R_MN0] == gmin) {
-        for (int i = 0; i < 6; ++i) s[21 + i] += (double)r[R_CMN + i];
-        s[27] += (double)r[R_NMN];
-      }
-      if (gmax != gmin && r[R_MX0] == gmax) {
-        for (int i = 0; i < 6; ++i) s[21 + i] += (double)r[R_CMX + i];
-        s[27] += (double)r[R_NMX];
-      }
-    }
-  }
-  __shared__ double sh[4][28];
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  for (int i = 0; i < 28; ++i) {
-    const double v = wave_sum_d(s[i]);
-    if (lane == 0) sh[wave][i] = v;
-  }
-  __syncthreads();
-  if (threadIdx.x != 0) return;
-  double tot[28];
-  for (int i = 0; i < 28; ++i) tot[i] = ((sh[0][i] + sh[1][i]) + sh[2][i]) + sh[3][i];
-  bool finite = true;
-  for (int i = 0; i < 27; ++i) finite = finite && isfinite(tot[i]);
-  if (!finite && q.status) atomicOr(q.status, DPFT_STATUS_NONFINITE);
-  if (q.jtj_out) {
-    int k = 0;
-    for (int i = 0; i < 6; ++i)
-      for (int j = i; j < 6; ++j) {
-        q.jtj_out[36 * b + 6 * i + j] = (float)tot[k];
-        q.jtj_out[36 * b + 6 * j + i] = (float)tot[k];
-        ++k;
-      }
-  }
-  if (q.jtr_out)
-    for (int i = 0; i < 6; ++i) q.jtr_out[6 * b + i] = (float)tot[21 + i];
-  if (q.invalid_out) q.invalid_out[b] = (int32_t)tot[27];
-  solve_and_update(tot, tot + 21, q.R + 9 * b, q.t + 3 * b);
-}
-
-__global__ __launch_bounds__(kThreads) void ic_loss_finalize_kernel(FinParams q) {
-  const int b = blockIdx.x;
-  const bool tru = (q.flags & DPFT_REMOVE_TRU_SIGMA) != 0;
-  float gmin = 0.f, gmax = 0.f;
-  if (tru) global_extrema(q.rec, q.nblocks, L_MN_ALL, L_MX_ALL, gmin, gmax);
-  double sum = 0.0, ninv = 0.0;
-  const int first = b * q.per_pair;
-  for (int k = threadIdx.x; k < q.per_pair; k += kThreads) {
-    const float* r = q.rec + (size_t)(first + k) * kRec;
-    sum += r[L_SUM];
-    ninv += r[L_NINV];
-    if (tru) {
-      if (r[L_MN0] == gmin) { sum -= r[L_LMN]; ninv += r[L_NMN]; }
-      if (gmax != gmin && r[L_MX0] == gmax) { sum -= r[L_LMX]; ninv += r[L_NMX]; }
-    }
-  }
-  __shared__ double sh[2][4];
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  sum = wave_sum_d(sum);
-  ninv = wave_sum_d(ninv);
-  if (lane == 0) {
-    sh[0][wave] = sum;
-    sh[1][wave] = ninv;
-  }
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    const double S = ((sh[0][0] + sh[0][1]) + sh[0][2]) + sh[0][3];
-    const double N = ((sh[1][0] + sh[1][1]) + sh[1][2]) + sh[1][3];
-    q.loss_out[b] = (float)(S / ((double)q.HW - N));
-  }
-}
-
-// sigma0 batch-global min / max (algorithms.py:1976-1977), order-preserving atomics.
-__global__ void ctrl_init_kernel(uint32_t* ctrl) {
-  ctrl[0] = 0xffffffffu;
-  ctrl[1] = 0u;
-}
-
+// sigma0 batch-global min / max (algorithms.py:1976-1977).  Per-workgroup
+// partials, the last workgroup reduces them in a fixed order (no atomics on data).
 __global__ __launch_bounds__(kThreads) void minmax_kernel(const float* __restrict__ s, size_t n, uint32_t* ctrl) {
+  __shared__ float sm[2][4];
   float mn = INFINITY, mx = -INFINITY;
   const size_t stride = (size_t)gridDim.x * kThreads;
   for (size_t i = (size_t)blockIdx.x * kThreads + threadIdx.x; i < n; i += stride) {
@@ -1018,9 +1188,33 @@ __global__ __launch_bounds__(kThreads) void minmax_kernel(const float* __restric
     mn = fminf(mn, __shfl_xor(mn, off));
     mx = fmaxf(mx, __shfl_xor(mx, off));
   }
-  if ((threadIdx.x & 63) == 0) {
-    atomicMin(&ctrl[0], enc_ord(mn));
-    atomicMax(&ctrl[1], enc_ord(mx));
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  if (lane == 0) {
+    sm[0][wave] = mn;
+    sm[1][wave] = mx;
+  }
+  __syncthreads();
+  float* part = reinterpret_cast<float*>(ctrl + kCtlPart);
+  if (threadIdx.x == 0) {
+    st_ag(part + 2 * blockIdx.x, fminf(fminf(sm[0][0], sm[0][1]), fminf(sm[0][2], sm[0][3])));
+    st_ag(part + 2 * blockIdx.x + 1, fmaxf(fmaxf(sm[1][0], sm[1][1]), fmaxf(sm[1][2], sm[1][3])));
+  }
+  if (!block_is_last(ctrl + kCtlMMDone, gridDim.x)) return;
+  if (threadIdx.x < 64) {
+    mn = INFINITY;
+    mx = -INFINITY;
+    for (int k = threadIdx.x; k < (int)gridDim.x; k += 64) {
+      mn = fminf(mn, ld_ag(part + 2 * k));
+      mx = fmaxf(mx, ld_ag(part + 2 * k + 1));
+    }
+    for (int off = 32; off > 0; off >>= 1) {
+      mn = fminf(mn, __shfl_xor(mn, off));
+      mx = fmaxf(mx, __shfl_xor(mx, off));
+    }
+    if (threadIdx.x == 0) {
+      ctrl[kCtlMin] = enc_ord(mn);
+      ctrl[kCtlMax] = enc_ord(mx);
+    }
   }
 }
 
@@ -1049,6 +1243,7 @@ int check_desc(const DpftLevelDesc* d) {
     return fail(DPFT_E_INVALID, "bad shape B=%d C=%d H=%d W=%d", d->B, d->C, d->H, d->W);
   if (d->Cs != 1 && d->Cs != d->C) return fail(DPFT_E_INVALID, "Cs must be 1 or C (got %d, C=%d)", d->Cs, d->C);
   if ((long)d->H * d->W >= (1L << 30)) return fail(DPFT_E_INVALID, "level too large");
+  if (d->B > kMaxPairs) return fail(DPFT_E_INVALID, "B=%d exceeds %d pairs per call", d->B, kMaxPairs);
   if (d->flags & DPFT_COMBINE_ICP) return fail(DPFT_E_INVALID, "COMBINE_ICP not supported by this build yet");
   return DPFT_OK;
 }
@@ -1059,9 +1254,12 @@ int check_tensors(const DpftLevelTensors* t) {
   return DPFT_OK;
 }
 
+// workspace: [ctrl][pair records B x kPRec fp64][workgroup records nblocks x kRec fp32]
+size_t prec_bytes(const DpftLevelDesc& d) { return ((size_t)d.B * kPRec * sizeof(double) + 255) & ~(size_t)255; }
+
 size_t ws_need(const DpftLevelDesc& d) {
   const Geometry g = plan(d);
-  return kCtrlBytes + (size_t)g.nblocks * kRec * sizeof(float);
+  return kCtrlBytes + prec_bytes(d) + (size_t)g.nblocks * kRec * sizeof(float);
 }
 
 IterParams make_params(const DpftLevelDesc& d, const DpftLevelTensors& tt, const Geometry& g, const float* R,
@@ -1088,8 +1286,19 @@ IterParams make_params(const DpftLevelDesc& d, const DpftLevelTensors& tt, const
   p.steps = g.steps;
   p.nblocks = g.nblocks;
   p.flags = d.flags;
-  p.ctrl = reinterpret_cast<const uint32_t*>(ws);
-  p.rec = reinterpret_cast<float*>(static_cast<char*>(ws) + kCtrlBytes);
+  p.ctrl = reinterpret_cast<uint32_t*>(ws);
+  p.rec = reinterpret_cast<float*>(static_cast<char*>(ws) + kCtrlBytes + prec_bytes(d));
+  p.fin_on = 0;
+  memset(&p.fin, 0, sizeof(p.fin));
+  p.fin.rec = p.rec;
+  p.fin.prec = reinterpret_cast<double*>(static_cast<char*>(ws) + kCtrlBytes);
+  p.fin.pair_cnt = p.ctrl + kCtlPair;
+  p.fin.done_cnt = p.ctrl + kCtlDone;
+  p.fin.nblocks = g.nblocks;
+  p.fin.per_pair = g.per_pair;
+  p.fin.HW = d.H * d.W;
+  p.fin.flags = d.flags;
+  p.fin.status = tt.status;
   return p;
 }
 
@@ -1100,11 +1309,10 @@ int hip_check(const char* what) {
 }
 
 int launch_minmax(const DpftLevelDesc& d, const DpftLevelTensors& tt, void* ws, hipStream_t st) {
+  if ((d.flags & DPFT_REMOVE_TRU_SIGMA) == 0) return DPFT_OK;  // extrema unused
   uint32_t* ctrl = reinterpret_cast<uint32_t*>(ws);
-  hipLaunchKernelGGL(ctrl_init_kernel, dim3(1), dim3(1), 0, st, ctrl);
-  if ((d.flags & DPFT_REMOVE_TRU_SIGMA) == 0) return hip_check("ctrl_init_kernel");
   const size_t n = (size_t)d.B * d.Cs * d.H * d.W;
-  const int grid = (int)std::min<size_t>((n + kThreads * 4 - 1) / (kThreads * 4), 2048);
+  const int grid = (int)std::min<size_t>((n + kThreads * 16 - 1) / (kThreads * 16), kMaxMMBlocks);
   hipLaunchKernelGGL(minmax_kernel, dim3(grid), dim3(kThreads), 0, st, tt.s0, n, ctrl);
   return hip_check("minmax_kernel");
 }
@@ -1144,23 +1352,14 @@ int iterate_impl(const DpftLevelDesc* desc, const DpftLevelTensors* tt, float* R
   if (ws_bytes < ws_need(*desc)) return fail(DPFT_E_WORKSPACE, "workspace %zu < %zu", ws_bytes, ws_need(*desc));
   const Geometry g = plan(*desc);
   if (first && (rc = launch_minmax(*desc, *tt, ws, st))) return rc;
-  const IterParams p = make_params(*desc, *tt, g, R, t, ws);
-  if ((rc = launch_reduce(p, st))) return rc;
-  FinParams q;
-  memset(&q, 0, sizeof(q));
-  q.rec = p.rec;
-  q.nblocks = g.nblocks;
-  q.per_pair = g.per_pair;
-  q.HW = desc->H * desc->W;
-  q.flags = desc->flags;
-  q.R = R;
-  q.t = t;
-  q.jtj_out = jtj_out;
-  q.jtr_out = jtr_out;
-  q.invalid_out = invalid_out;
-  q.status = tt->status;
-  hipLaunchKernelGGL(ic_finalize_kernel, dim3(desc->B), dim3(kThreads), 0, st, q);
-  return hip_check("ic_finalize_kernel");
+  IterParams p = make_params(*desc, *tt, g, R, t, ws);
+  p.fin_on = 1;
+  p.fin.R = R;
+  p.fin.t = t;
+  p.fin.jtj_out = jtj_out;
+  p.fin.jtr_out = jtr_out;
+  p.fin.invalid_out = invalid_out;
+  return launch_reduce(p, st);
 }
 
 }  // namespace
@@ -1202,23 +1401,13 @@ int dpft_ic_residual_level(const DpftLevelDesc* desc, const DpftLevelTensors* tt
   hipStream_t st = static_cast<hipStream_t>(hip_stream);
   const Geometry g = plan(*desc);
   if ((rc = launch_minmax(*desc, *tt, ws, st))) return rc;
-  const IterParams p = make_params(*desc, *tt, g, R, t, ws);
+  IterParams p = make_params(*desc, *tt, g, R, t, ws);
+  p.fin.loss_out = loss;
   if (p.Cs == 1)
     hipLaunchKernelGGL(ic_residual_kernel<true>, dim3(p.nblocks), dim3(kThreads), 0, st, p);
   else
     hipLaunchKernelGGL(ic_residual_kernel<false>, dim3(p.nblocks), dim3(kThreads), 0, st, p);
-  if ((rc = hip_check("ic_residual_kernel"))) return rc;
-  FinParams q;
-  memset(&q, 0, sizeof(q));
-  q.rec = p.rec;
-  q.nblocks = g.nblocks;
-  q.per_pair = g.per_pair;
-  q.HW = desc->H * desc->W;
-  q.flags = desc->flags;
-  q.loss_out = loss;
-  q.status = tt->status;
-  hipLaunchKernelGGL(ic_loss_finalize_kernel, dim3(desc->B), dim3(kThreads), 0, st, q);
-  return hip_check("ic_loss_finalize_kernel");
+  return hip_check("ic_residual_kernel");
 }
 
 int dpft_ic_reduce_only(const DpftLevelDesc* desc, const DpftLevelTensors* tt, const float* R, const float* t,

@@ -23,7 +23,8 @@ def _workspace(device, nbytes):
     key = (device.type, device.index)
     buf = _ws_cache.get(key)
     if buf is None or buf.numel() < nbytes:
-        buf = torch.empty(max(nbytes, 1 << 20), dtype=torch.uint8, device=device)
+        # zero-filled once: the library's completion counters live in it (dpft_ic.h)
+        buf = torch.zeros(max(nbytes, 1 << 20), dtype=torch.uint8, device=device)
         _ws_cache[key] = buf
     return buf
 
@@ -183,7 +184,7 @@ class PyramidSolver:
                                         depth0=d.get("depth0"), depth1=d.get("depth1"), combine_icp=combine_icp,
                                         icp_weight=icp_weight, status=self.status))
         nbytes = max(c.ws_bytes for c in self.calls)
-        self.ws = torch.empty(nbytes, dtype=torch.uint8, device=dev)  # private: safe to capture
+        self.ws = torch.zeros(nbytes, dtype=torch.uint8, device=dev)  # private: safe to capture; zeroed (counters)
         self.ws_bytes = nbytes
         self.device = dev
         self.B = self.calls[0].B
@@ -196,6 +197,16 @@ class PyramidSolver:
             rc = L.dpft_ic_solve_level(ctypes.byref(c.desc), ctypes.byref(c.tens), _ptr(R), _ptr(t), None, None,
                                        _ptr(self.ws), self.ws_bytes, st)
             N.check(rc, "dpft_ic_solve_level")
+
+    def iterate(self, level, R, t, first=False):
+        """One full iteration (fused reduce + in-kernel finalize) of `level`, in place.
+
+        With first=False it reuses the sigma0 extrema the last pass over this level left
+        in the workspace; bench.py times the dominant kernel this way."""
+        c = self.calls[level]
+        rc = N.lib().dpft_ic_iterate(ctypes.byref(c.desc), ctypes.byref(c.tens), _ptr(R), _ptr(t), None, None, None,
+                                     int(first), _ptr(self.ws), self.ws_bytes, _stream(self.device))
+        N.check(rc, "dpft_ic_iterate")
 
     def reduce_only(self, level, R, t):
         """Launch only the fused residual/Jacobian/JtJ kernel of `level` (roofline timing)."""

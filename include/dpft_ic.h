@@ -90,7 +90,10 @@ typedef struct DpftLevelTensors {
     uint32_t* status;     /* [1]        device status word, OR-ed, never cleared */
 } DpftLevelTensors;
 
-/* Bytes of workspace the level needs (>= 256-byte aligned pointer expected). */
+/* Bytes of workspace the level needs (>= 256-byte aligned pointer expected).
+ * The workspace must be ZERO-FILLED before its first use (hipMemsetAsync):
+ * it holds the completion counters of the in-kernel finalize, which every call
+ * leaves at zero again.  One workspace serves one stream at a time. */
 size_t dpft_workspace_size(const DpftLevelDesc* desc);
 
 /*
