@@ -49,6 +49,8 @@
 #include <cstdint>
 #include <cstdio>
 #include <cstring>
+#include <mutex>
+#include <vector>
 
 #include "dpft_ic.h"
 
@@ -100,6 +102,7 @@ constexpr int L_SUM = 0, L_NINV = 1, L_MN_ALL = 2, L_MN0 = 3, L_LMN = 4, L_NMN =
 constexpr int kCtlMin = 0, kCtlMax = 1, kCtlDone = 2, kCtlMMDone = 3, kCtlResDone = 4, kCtlPart = 64, kCtlPair = 1152;
 constexpr int kMaxMMBlocks = 512;
 constexpr int kMaxPairs = 2048;  // per call (one completion counter per pair)
+constexpr int kMaxGrid = 4096;   // reduce-kernel workgroups (resident capacity is far below)
 constexpr size_t kCtrlBytes = 16384;
 static_assert((kCtlPart + 2 * kMaxMMBlocks) * 4 <= kCtlPair * 4, "ctrl area");
 static_assert((kCtlPair + kMaxPairs) * 4 <= kCtrlBytes, "ctrl area");
@@ -148,13 +151,13 @@ __device__ __forceinline__ T ld_ag(const T* p) {
   return __hip_atomic_load(const_cast<T*>(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
-__device__ bool block_is_last(uint32_t* counter, uint32_t total) {
+__device__ bool block_is_last(uint32_t* counter, uint32_t add, uint32_t total) {
   __shared__ int s_last;
   __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0): this wave's stores are complete
   __syncthreads();
   if (threadIdx.x == 0) {
-    const uint32_t prev = __hip_atomic_fetch_add(counter, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    const int last = prev == total - 1u;
+    const uint32_t prev = __hip_atomic_fetch_add(counter, add, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const int last = prev + add == total;
     if (last) st_ag(counter, 0u);  // ready for the next launch
     s_last = last;
   }
@@ -254,6 +257,7 @@ __device__ __forceinline__ Warp warp_point(int x, int y, float d, const float* _
 // Last-block finalize parameters (one record per workgroup, fixed-order fp64 sums).
 struct FinParams {
   const float* rec;
+  int nbpp, B;        // reduce kernel: workgroups (records) per pair, pairs
   double* prec;       // [B][kPRec] per-pair records
   uint32_t* pair_cnt; // [B] completion counters
   uint32_t* done_cnt; // pairs finished
@@ -283,8 +287,10 @@ struct IterParams {
   int B, C, Cs, H, W;
   int tiles_x, tiles_y, steps, nblocks;
   uint32_t flags;
-  uint32_t* ctrl;  // see kCtl*
+  uint32_t* ctrl;        // see kCtl*
+  const uint32_t* ext;   // sigma0 extrema of this level (order-encoded min, max)
   float* rec;
+  int nbpp, per_pair, row_groups;  // reduce kernel schedule (see ic_reduce_kernel)
   int fin_on;      // 0: records only (timing hook); 1: last workgroup finalizes
   FinParams fin;
 };
@@ -608,8 +614,8 @@ __device__ void pair_reduce(const FinParams& q, int b) {
   __shared__ double part[8][32], pmn[8][8], pmx[8][8];
   const int tid = threadIdx.x, i = tid & 31, j = tid >> 5;
   const bool tru = (q.flags & DPFT_REMOVE_TRU_SIGMA) != 0;
-  const float* rec = q.rec + (size_t)b * q.per_pair * kRec;
-  const int n = q.per_pair;
+  const float* rec = q.rec + (size_t)b * q.nbpp * kRec;  // slots of pair b's workgroups
+  const int n = q.nbpp;
   float mn_all = INFINITY, mx_all = -INFINITY, mn0 = INFINITY, mx0 = -INFINITY;
   if (tru) {
     float a = INFINITY, c = -INFINITY;
@@ -687,7 +693,7 @@ __device__ void pair_reduce(const FinParams& q, int b) {
 // updates its pose (algorithms.py:2017-2103).
 __device__ void finalize_batch(const FinParams& q) {
   const bool tru = (q.flags & DPFT_REMOVE_TRU_SIGMA) != 0;
-  const int B = q.nblocks / q.per_pair;
+  const int B = q.B;
   float gmin = INFINITY, gmax = -INFINITY, u0 = INFINITY, u1 = -INFINITY;
   if (tru) {
     for (int b = threadIdx.x; b < B; b += kThreads) {
@@ -761,6 +767,13 @@ __device__ void finalize_loss(const FinParams& q) {
 // Loads of channel chunk k+1 are issued before chunk k's math; chunks go in
 // (even, odd) pairs so each load set lives in fixed registers and no in-flight
 // load is ever copied (a copy would force the wait the prefetch exists to avoid).
+// Work split: a pair's level is tiles_x * row_groups tiles of 4 rows x 62
+// columns, ordered (column strip, row group).  Each pair gets nbpp workgroups
+// (B * nbpp ~ the device's resident capacity: no tail round) and workgroup j of
+// pair b takes the contiguous tile range [n j / nbpp, n (j+1) / nbpp): one
+// prologue / epilogue per workgroup, and consecutive tiles are vertically
+// adjacent, so the halo rows of f0 / sigma0 are re-read from L2 right after
+// their first use.  Workgroup k writes record slot k.
 template <int CT, bool CS1, bool TRU>
 __global__ __launch_bounds__(kThreads, DPFT_MIN_WAVES) void ic_reduce_kernel(IterParams p) {
   const int C = CT > 0 ? CT : p.C;
@@ -768,12 +781,21 @@ __global__ __launch_bounds__(kThreads, DPFT_MIN_WAVES) void ic_reduce_kernel(Ite
   __shared__ float red[4][kRec];
 
   const int tid = threadIdx.x, lane = tid & 63, wave = wave_id();
-  const int bid = xcd_remap(blockIdx.x, p.nblocks);
-  const int tx = bid % p.tiles_x;
-  const int rest = bid / p.tiles_x;
-  const int ty = rest % p.tiles_y;
-  const int b = rest / p.tiles_y;
   const int W = p.W, H = p.H, HW = H * W;
+#ifndef DPFT_REMAP
+#define DPFT_REMAP 1
+#endif
+#ifndef DPFT_ORDER
+#define DPFT_ORDER 1
+#endif
+  const int kb = DPFT_REMAP ? xcd_remap(blockIdx.x, gridDim.x) : blockIdx.x;
+  const int b = kb / p.nbpp, jb = kb - b * p.nbpp;
+  const int seg_begin = b * p.per_pair + (int)(((long)p.per_pair * jb) / p.nbpp);
+  const int seg_end = b * p.per_pair + (int)(((long)p.per_pair * (jb + 1)) / p.nbpp);
+  const float g0min = TRU ? dec_ord(p.ext[0]) : 0.f, g0max = TRU ? dec_ord(p.ext[1]) : 0.f;
+  const uint32_t planeB = (uint32_t)HW * 4u;
+  const int nch = (C + kCK - 1) / kCK;
+  const int npair = (nch + 1) >> 1;                 // chunk pairs per step (odd counts get an empty chunk)
 
   const float fx = p.K[4 * b + 0], fy = p.K[4 * b + 1], cx = p.K[4 * b + 2], cy = p.K[4 * b + 3];
   float Rm[9], tv[3];
@@ -781,9 +803,7 @@ __global__ __launch_bounds__(kThreads, DPFT_MIN_WAVES) void ic_reduce_kernel(Ite
   for (int k = 0; k < 9; ++k) Rm[k] = p.R[9 * b + k];
 #pragma unroll
   for (int k = 0; k < 3; ++k) tv[k] = p.t[3 * b + k];
-  const float g0min = TRU ? dec_ord(p.ctrl[0]) : 0.f, g0max = TRU ? dec_ord(p.ctrl[1]) : 0.f;
 
-  const uint32_t planeB = (uint32_t)HW * 4u;
   const auto rf0 = rsrc(p.f0 + (size_t)b * C * HW, planeB * C);
   const auto rf1 = rsrc(p.f1 + (size_t)b * C * HW, planeB * C);
   const auto rs0 = rsrc(p.s0 + (size_t)b * p.Cs * HW, planeB * p.Cs);
@@ -803,21 +823,41 @@ __global__ __launch_bounds__(kThreads, DPFT_MIN_WAVES) void ic_reduce_kernel(Ite
     for (int k = 0; k < 14; ++k) lds_ext[k][tid] = 0.0f;
   }
 
-  const int xs = tx * kTileOut - 1 + lane;          // this lane's image column (may be -1 or >= W)
-  const int xc = min(max(xs, 0), W - 1);            // clamped: replicate padding of the stencil
-  const bool out_lane = (lane >= 1) && (lane <= kTileOut) && (xs < W);
-  const int colv = xc * 4;
-  const int nch = (C + kCK - 1) / kCK;
-  const int npair = (nch + 1) >> 1;                 // chunk pairs per step (odd counts get an empty chunk)
-  const int yb = ty * p.steps * kRowsPerStep;
-
-  float d_cur = bld(rd0, min(yb + wave, H - 1) * W * 4 + colv, 0);
-  for (int s = 0; s < p.steps; ++s) {
-    const int y = yb + s * kRowsPerStep + wave;
-    if (__builtin_amdgcn_readfirstlane(y) >= H) break;  // wave-uniform: this wave's rows are done
+  // tile -> (column strip, row of this wave); rows past H are clamped for the
+  // prefetch and skipped by the wave (wave-uniform)
+  auto tile_pos = [&](int i, int& xs, int& y) {
+    const int local = i - b * p.per_pair;
+#if DPFT_ORDER == 0
+    const int tx = local / p.row_groups;
+    y = (local - tx * p.row_groups) * kRowsPerStep + wave;
+#else
+    const int ty = local / p.tiles_x;
+    const int tx = local - ty * p.tiles_x;
+    y = ty * kRowsPerStep + wave;
+#endif
+    xs = tx * kTileOut - 1 + lane;                  // this lane's image column (may be -1 or >= W)
+  };
+  float d_cur;
+  {
+    int xs0, y0;
+    tile_pos(seg_begin, xs0, y0);
+    d_cur = bld(rd0, min(y0, H - 1) * W * 4 + min(max(xs0, 0), W - 1) * 4, 0);
+  }
+  for (int it = seg_begin; it < seg_end; ++it) {
+    int xs, y;
+    tile_pos(it, xs, y);
+    const int xc = min(max(xs, 0), W - 1);          // clamped: replicate padding of the stencil
+    const bool out_lane = (lane >= 1) && (lane <= kTileOut) && (xs < W);
+    const int colv = xc * 4;
+    const float d = d_cur;
+    if (it + 1 < seg_end) {
+      int xn, yn;
+      tile_pos(it + 1, xn, yn);
+      d_cur = bld(rd0, min(yn, H - 1) * W * 4 + min(max(xn, 0), W - 1) * 4, 0);
+    }
+    if (__builtin_amdgcn_readfirstlane(y) >= H) continue;  // wave-uniform: row past the image
     const int rT = max(y - 1, 0) * W * 4, rM = y * W * 4, rB = min(y + 1, H - 1) * W * 4;
     // ---- frame: warp, taps, occlusion, masks (geometry.py:291-350, algorithms.py:1999-2008)
-    const float d = d_cur;
     const Warp wp = warp_point(xc, y, d, Rm, tv, fx, fy, cx, cy);
     const Taps tp = make_taps(wp.u, wp.v, H, W);
     const Gather4 gd1 = gather4(rd1, tp, 0);
@@ -831,7 +871,6 @@ __global__ __launch_bounds__(kThreads, DPFT_MIN_WAVES) void ic_reduce_kernel(Ite
       s0b_ = bld(rs0, colv, rB);
       gs1 = gather4(rs1, tp, 0);
     }
-    if (s + 1 < p.steps) d_cur = bld(rd0, min(y + kRowsPerStep, H - 1) * W * 4 + colv, 0);
 
     ChanLoads LE[kCK], LO[kCK];
     auto issue = [&](ChanLoads (&L)[kCK], int k) {
@@ -1018,7 +1057,7 @@ __global__ __launch_bounds__(kThreads, DPFT_MIN_WAVES) void ic_reduce_kernel(Ite
     }
   }
   __syncthreads();
-  float* out = p.rec + (size_t)bid * kRec;
+  float* out = p.rec + (size_t)kb * kRec;
   if (tid < 28) {
     st_ag(out + tid, (float)(((red[0][tid] + red[1][tid]) + red[2][tid]) + red[3][tid]));
   } else if (TRU && tid == 64) {
@@ -1044,9 +1083,10 @@ __global__ __launch_bounds__(kThreads, DPFT_MIN_WAVES) void ic_reduce_kernel(Ite
     st_ag(out + R_NMX, (float)(e.n));
     for (int k = 0; k < 6; ++k) st_ag(out + R_CMX + k, (float)(e.c[k]));
   }
-  if (p.fin_on && block_is_last(p.fin.pair_cnt + b, (uint32_t)(p.tiles_x * p.tiles_y))) {
+  // the last workgroup of a pair reduces its records; the one completing the batch solves
+  if (p.fin_on && block_is_last(p.fin.pair_cnt + b, 1u, (uint32_t)p.nbpp)) {
     pair_reduce(p.fin, b);
-    if (block_is_last(p.fin.done_cnt, (uint32_t)p.B)) finalize_batch(p.fin);
+    if (block_is_last(p.fin.done_cnt, 1u, (uint32_t)p.B)) finalize_batch(p.fin);
   }
 }
 
@@ -1066,7 +1106,7 @@ __global__ __launch_bounds__(kThreads) void ic_residual_kernel(IterParams p) {
   float Rm[9], tv[3];
   for (int k = 0; k < 9; ++k) Rm[k] = p.R[9 * b + k];
   for (int k = 0; k < 3; ++k) tv[k] = p.t[3 * b + k];
-  const float g0min = dec_ord(p.ctrl[0]), g0max = dec_ord(p.ctrl[1]);
+  const float g0min = dec_ord(p.ext[0]), g0max = dec_ord(p.ext[1]);
   const float* f0b = p.f0 + (size_t)b * C * HW;
   const float* f1b = p.f1 + (size_t)b * C * HW;
   const float* s0b = p.s0 + (size_t)b * p.Cs * HW;
@@ -1145,7 +1185,7 @@ __global__ __launch_bounds__(kThreads) void ic_residual_kernel(IterParams p) {
     st_ag(out + L_MN_ALL, (float)(ma)); st_ag(out + L_MN0, (float)(m0)); st_ag(out + L_LMN, (float)(lm)); st_ag(out + L_NMN, (float)(nm));
     st_ag(out + L_MX_ALL, (float)(xa)); st_ag(out + L_MX0, (float)(x0v)); st_ag(out + L_LMX, (float)(lx)); st_ag(out + L_NMX, (float)(nx));
   }
-  if (block_is_last(p.ctrl + kCtlResDone, (uint32_t)p.nblocks)) finalize_loss(p.fin);
+  if (block_is_last(p.ctrl + kCtlResDone, 1u, (uint32_t)p.nblocks)) finalize_loss(p.fin);
 }
 
 
@@ -1199,7 +1239,7 @@ __global__ __launch_bounds__(kThreads) void minmax_kernel(const float* __restric
     st_ag(part + 2 * blockIdx.x, fminf(fminf(sm[0][0], sm[0][1]), fminf(sm[0][2], sm[0][3])));
     st_ag(part + 2 * blockIdx.x + 1, fmaxf(fmaxf(sm[1][0], sm[1][1]), fmaxf(sm[1][2], sm[1][3])));
   }
-  if (!block_is_last(ctrl + kCtlMMDone, gridDim.x)) return;
+  if (!block_is_last(ctrl + kCtlMMDone, 1u, gridDim.x)) return;
   if (threadIdx.x < 64) {
     mn = INFINITY;
     mx = -INFINITY;
@@ -1257,9 +1297,11 @@ int check_tensors(const DpftLevelTensors* t) {
 // workspace: [ctrl][pair records B x kPRec fp64][workgroup records nblocks x kRec fp32]
 size_t prec_bytes(const DpftLevelDesc& d) { return ((size_t)d.B * kPRec * sizeof(double) + 255) & ~(size_t)255; }
 
+// reduce-kernel record slots: B * nbpp <= max(kMaxGrid, B)
 size_t ws_need(const DpftLevelDesc& d) {
   const Geometry g = plan(d);
-  return kCtrlBytes + prec_bytes(d) + (size_t)g.nblocks * kRec * sizeof(float);
+  const size_t slots = std::max<size_t>(std::max<size_t>(kMaxGrid, d.B), (size_t)g.nblocks);
+  return kCtrlBytes + prec_bytes(d) + slots * kRec * sizeof(float);
 }
 
 IterParams make_params(const DpftLevelDesc& d, const DpftLevelTensors& tt, const Geometry& g, const float* R,
@@ -1287,7 +1329,11 @@ IterParams make_params(const DpftLevelDesc& d, const DpftLevelTensors& tt, const
   p.nblocks = g.nblocks;
   p.flags = d.flags;
   p.ctrl = reinterpret_cast<uint32_t*>(ws);
+  p.ext = p.ctrl + kCtlMin;
   p.rec = reinterpret_cast<float*>(static_cast<char*>(ws) + kCtrlBytes + prec_bytes(d));
+  p.row_groups = (d.H + kRowsPerStep - 1) / kRowsPerStep;
+  p.per_pair = g.tiles_x * p.row_groups;
+  p.nbpp = 0;  // set at launch from the kernel's resident capacity
   p.fin_on = 0;
   memset(&p.fin, 0, sizeof(p.fin));
   p.fin.rec = p.rec;
@@ -1299,6 +1345,7 @@ IterParams make_params(const DpftLevelDesc& d, const DpftLevelTensors& tt, const
   p.fin.HW = d.H * d.W;
   p.fin.flags = d.flags;
   p.fin.status = tt.status;
+  p.fin.B = d.B;
   return p;
 }
 
@@ -1317,29 +1364,62 @@ int launch_minmax(const DpftLevelDesc& d, const DpftLevelTensors& tt, void* ws, 
   return hip_check("minmax_kernel");
 }
 
+// Workgroups of `kernel` the current device holds at once (cached per kernel and device).
+int resident_blocks(const void* kernel) {
+  struct Entry {
+    const void* k;
+    int dev, n;
+  };
+  static std::mutex mu;
+  static std::vector<Entry> cache;
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess) return 0;
+  std::lock_guard<std::mutex> lock(mu);
+  for (const Entry& e : cache)
+    if (e.k == kernel && e.dev == dev) return e.n;
+  int per_cu = 0, cus = 0;
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kernel, kThreads, 0) != hipSuccess ||
+      hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
+    return 0;
+  const int n = std::max(1, std::min(per_cu * cus, kMaxGrid));
+  cache.push_back({kernel, dev, n});
+  return n;
+}
+
+template <int CT, bool CS1, bool TRU>
+int launch_reduce_k(IterParams p, hipStream_t st) {
+  const void* k = reinterpret_cast<const void*>(&ic_reduce_kernel<CT, CS1, TRU>);
+  const int cap = resident_blocks(k);
+  if (cap <= 0) return fail(DPFT_E_HIP, "occupancy query failed");
+  p.nbpp = std::max(1, std::min(cap / p.B, p.per_pair));
+  p.fin.nbpp = p.nbpp;
+  hipLaunchKernelGGL((ic_reduce_kernel<CT, CS1, TRU>), dim3(p.B * p.nbpp), dim3(kThreads), 0, st, p);
+  return DPFT_OK;
+}
+
 template <int CT, bool CS1>
-void launch_reduce_t(const IterParams& p, hipStream_t st) {
-  if (p.flags & DPFT_REMOVE_TRU_SIGMA)
-    hipLaunchKernelGGL((ic_reduce_kernel<CT, CS1, true>), dim3(p.nblocks), dim3(kThreads), 0, st, p);
-  else
-    hipLaunchKernelGGL((ic_reduce_kernel<CT, CS1, false>), dim3(p.nblocks), dim3(kThreads), 0, st, p);
+int launch_reduce_t(const IterParams& p, hipStream_t st) {
+  return (p.flags & DPFT_REMOVE_TRU_SIGMA) ? launch_reduce_k<CT, CS1, true>(p, st)
+                                           : launch_reduce_k<CT, CS1, false>(p, st);
 }
 
 int launch_reduce(const IterParams& p, hipStream_t st) {
+  int rc;
   if (p.Cs == 1) {
     switch (p.C) {
-      case 8: launch_reduce_t<8, true>(p, st); break;
-      case 16: launch_reduce_t<16, true>(p, st); break;
-      case 32: launch_reduce_t<32, true>(p, st); break;
-      default: launch_reduce_t<0, true>(p, st); break;
+      case 8: rc = launch_reduce_t<8, true>(p, st); break;
+      case 16: rc = launch_reduce_t<16, true>(p, st); break;
+      case 32: rc = launch_reduce_t<32, true>(p, st); break;
+      default: rc = launch_reduce_t<0, true>(p, st); break;
     }
   } else {
     switch (p.C) {
-      case 8: launch_reduce_t<8, false>(p, st); break;
-      case 32: launch_reduce_t<32, false>(p, st); break;
-      default: launch_reduce_t<0, false>(p, st); break;
+      case 8: rc = launch_reduce_t<8, false>(p, st); break;
+      case 32: rc = launch_reduce_t<32, false>(p, st); break;
+      default: rc = launch_reduce_t<0, false>(p, st); break;
     }
   }
+  if (rc) return rc;
   return hip_check("ic_reduce_kernel");
 }
 

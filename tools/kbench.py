@@ -16,27 +16,31 @@ p = argparse.ArgumentParser()
 p.add_argument("--level", type=int, default=0)
 p.add_argument("--batch", type=int, default=8)
 p.add_argument("--reps", type=int, default=20)
+p.add_argument("--mode", choices=["reduce", "iterate"], default="reduce")
 a = p.parse_args()
 dev = torch.device("cuda:0")
 sel, levels, K = bench.make_inputs(a.batch, 0, dev)
 solver = ic.PyramidSolver(levels, K, iters=3, remove_tru_sigma=True)
 R = torch.eye(3, device=dev).repeat(a.batch, 1, 1).contiguous()
 t = torch.zeros(a.batch, 3, device=dev)
-c = solver.calls[a.level]
 import ctypes
 from deep_prob_feature_track_amd import _native as N
-rc = N.lib().dpft_ic_iterate(ctypes.byref(c.desc), ctypes.byref(c.tens), ic._ptr(R.clone()), ic._ptr(t.clone()),
-                             None, None, None, 1, ic._ptr(solver.ws), solver.ws_bytes, ic._stream(dev))
-N.check(rc, "iterate")  # leaves this level's sigma0 extrema in the workspace
-torch.cuda.synchronize()
-for _ in range(3):
-    solver.reduce_only(a.level, R, t)
-e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-e0.record()
-for _ in range(a.reps):
-    solver.reduce_only(a.level, R, t)
-e1.record()
-torch.cuda.synchronize()
-us = e0.elapsed_time(e1) / a.reps * 1e3
-gb = solver.algorithmic_bytes(a.level) / (us * 1e-6) / 1e9
-print(f"level {a.level} B={a.batch}: {us:.1f} us/launch, {gb:.0f} GB/s algorithmic ({gb / 8000 * 100:.1f}% of 8 TB/s)")
+for level in ([a.level] if a.level >= 0 else range(len(solver.calls))):
+    c = solver.calls[level]
+    rc = N.lib().dpft_ic_iterate(ctypes.byref(c.desc), ctypes.byref(c.tens), ic._ptr(R.clone()), ic._ptr(t.clone()),
+                                 None, None, None, 1, ic._ptr(solver.ws), solver.ws_bytes, ic._stream(dev))
+    N.check(rc, "iterate")  # leaves this level's sigma0 extrema in the workspace
+    torch.cuda.synchronize()
+    run = (lambda: solver.reduce_only(level, R, t)) if a.mode == "reduce" else (lambda: solver.iterate(level, R, t))
+    for _ in range(3):
+        run()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    for _ in range(a.reps):
+        run()
+    e1.record()
+    torch.cuda.synchronize()
+    us = e0.elapsed_time(e1) / a.reps * 1e3
+    gbs = solver.algorithmic_bytes(level) / (us * 1e-6) / 1e9
+    print(f"{os.path.basename(os.environ.get('DPFT_LIB', 'libdpft_ic.so'))} {a.mode} level {level} B={a.batch}: "
+          f"{us:.1f} us/launch, {gbs:.0f} GB/s algorithmic ({gbs / 80:.1f}% of 8 TB/s)", flush=True)
