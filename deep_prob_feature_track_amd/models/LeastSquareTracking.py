@@ -1,0 +1,208 @@
+"""Drop-in `LeastSquareTracking` (reference: code/models/LeastSquareTracking.py).
+
+Same constructor arguments and `options` attributes (LeastSquareTracking.py:
+38-103), same attributes (`tr_update0..3`, `track_type`, `scales`, `encoder`,
+`pose_predictor`, ...), same state_dict keys, same `forward` /
+`compute_residual` signatures and return values.  The coarse-to-fine solve runs
+on libdpft_ic.so through `TrustRegionInverseWUncertainty`; the encoder and
+init-pose networks run as PyTorch modules on the same device.
+
+Supported: track_type 'U_IC' (uncertainty_type != 'None', direction 'inverse')
+with encoders RGB / ConvRGBD / ConvRGBD2, identity or learned init pose,
+remove_tru_sigma, uncer_prop (returns JtWJ) and object masks, inference mode.
+The reference's other trackers (IC, U_FC, ICP) and training-mode forward raise
+NotImplementedError -- the reference itself cannot train on torch 2.x
+(algorithms.py:874-875).  Visualisation / logging arguments are accepted and
+ignored (they only draw with cv2 / tensorboard).
+"""
+import types
+
+import torch
+import torch.nn as nn
+
+from .algorithms import (DeepRobustEstimator, DirectSolverNet, FeaturePyramid, ImagePyramids, PoseNet, ScaleNet,
+                         SFMPoseNet, TrustRegionInverseWUncertainty)
+from .submodules import color_normalize
+
+# options attributes the reference constructor reads, with config.py's defaults
+DEFAULT_OPTIONS = dict(vis_feat=False, train_uncer_prop=False, combine_ICP=False, feature_extract='average',
+                       feature_channel=1, uncertainty_channel=1, scaler='None', remove_tru_sigma=False,
+                       init_pose='identity', train_init_pose=False, scale_init_pose=0.01, multi_hypo='None',
+                       res_input=False, checkpoint='')
+
+
+def default_options(**overrides):
+    """A namespace with every `options` attribute the constructor reads."""
+    d = dict(DEFAULT_OPTIONS)
+    d.update(overrides)
+    return types.SimpleNamespace(**d)
+
+
+class LeastSquareTracking(nn.Module):
+    NONE = -1
+    RGB = 0
+    CONV_RGBD = 1
+    CONV_RGBD2 = 2
+
+    def __init__(self, encoder_name, uncertainty_type, max_iter_per_pyr, mEst_type, solver_type, tr_samples=10,
+                 direction='inverse', options=None, vis_res=False, add_init_noise=False, no_weight_sharing=False,
+                 init_pose_type=None, feature_channel=None, uncertainty_channel=None, remove_tru_sigma=None,
+                 feature_extract=None, combine_ICP=None, scaler=None, scale_scaler=None, timers=None):
+        super().__init__()
+        if options is None:
+            options = default_options()
+        self.scales = [0, 1, 2, 3]
+        self.construct_image_pyramids = ImagePyramids(self.scales, pool='avg')
+        self.construct_depth_pyramids = ImagePyramids(self.scales, pool='max')
+        self.timers = timers
+        self.direction = direction
+        self.mEst_type = mEst_type
+        self.vis_res = vis_res
+        self.add_init_noise = add_init_noise
+
+        pick = lambda arg, name: getattr(options, name) if arg is None else arg  # noqa: E731
+        self.vis_feat_uncer = options.vis_feat
+        self.uncer_prop = options.train_uncer_prop
+        self.combine_icp = pick(combine_ICP, 'combine_ICP')
+        feature_extract = pick(feature_extract, 'feature_extract')
+        self.uncertainty_type = uncertainty_type
+        feature_channel = pick(feature_channel, 'feature_channel')
+        uncertainty_channel = pick(uncertainty_channel, 'uncertainty_channel')
+        scale_type = pick(scaler, 'scaler')
+        remove_tru_sigma = pick(remove_tru_sigma, 'remove_tru_sigma')
+        init_pose_type = pick(init_pose_type, 'init_pose')
+        self.predict_init_pose = init_pose_type != 'identity'
+        self.train_init_pose = options.train_init_pose
+        self.checkpoint = options.checkpoint
+
+        # ---- feature encoder (LeastSquareTracking.py:105-139)
+        if encoder_name in ('RGB', 'ICP'):
+            self.encoder = None
+            self.encoder_type = self.RGB
+        elif encoder_name in ('ConvRGBD', 'ConvRGBD2'):
+            self.encoder_type = self.CONV_RGBD if encoder_name == 'ConvRGBD' else self.CONV_RGBD2
+            self.encoder = FeaturePyramid(D=4 if encoder_name == 'ConvRGBD' else 8, w_uncertainty=uncertainty_type,
+                                          feature_channel=feature_channel, feature_extract=feature_extract,
+                                          uncertainty_channel=uncertainty_channel)
+        else:
+            raise NotImplementedError()
+
+        # ---- per-level helper modules, shared unless no_weight_sharing (143-197)
+        def per_level(attr, make):
+            if no_weight_sharing:
+                mods = [make() for _ in range(4)]
+                for i, m in enumerate(mods):
+                    setattr(self, f'{attr}{i}', m)
+                return mods
+            m = make()
+            setattr(self, attr, m)
+            return [m] * 4
+
+        scaler_funcs = per_level('scaler_func', lambda: ScaleNet(scale_type, scale=scale_scaler))
+        mEst_funcs = per_level('mEst_func', lambda: DeepRobustEstimator(mEst_type))
+        solver_funcs = per_level('solver_func', lambda: DirectSolverNet(solver_type, samples=tr_samples,
+                                                                        direction=direction))
+
+        # ---- trust-region solver per level (203-291)
+        if uncertainty_type == 'ICP':
+            self.track_type = 'ICP'
+        elif uncertainty_type == 'None' and direction == 'inverse':
+            self.track_type = 'IC'
+        elif uncertainty_type != 'None' and direction == 'forward':
+            self.track_type = 'U_FC'
+        elif uncertainty_type != 'None' and direction == 'inverse':
+            self.track_type = 'U_IC'
+        else:
+            raise NotImplementedError("Not supported tracking method, check again about the configs of "
+                                      "uncertainty and direction.")
+        if self.track_type != 'U_IC':
+            raise NotImplementedError(f"track type {self.track_type}: this build implements the U_IC solver only")
+        for i in range(4):
+            setattr(self, f'tr_update{i}', TrustRegionInverseWUncertainty(
+                max_iter_per_pyr, mEst_func=mEst_funcs[i], solver_func=solver_funcs[i], timers=timers,
+                combine_icp=self.combine_icp, scale_func=scaler_funcs[i], uncer_prop=options.train_uncer_prop,
+                remove_tru_sigma=remove_tru_sigma))
+
+        # ---- init-pose network (295-309)
+        if self.predict_init_pose:
+            nets = {'sfm_net': SFMPoseNet, 'dense_net': PoseNet}
+            if init_pose_type not in nets:
+                raise NotImplementedError('unsupported pose predictor network')
+            self.pose_predictor = nets[init_pose_type](scale_motion=options.scale_init_pose,
+                                                       multi_hypo=options.multi_hypo, res_input=options.res_input)
+
+    # ------------------------------------------------------------------ API
+    def forward(self, img0, img1, depth0, depth1, K, init_only=False, logger=None, iteration=0, vis=False,
+                obj_mask0=None, obj_mask1=None, index=None):
+        """Coarse-to-fine U_IC tracking (LeastSquareTracking.py:311-577); returns [R, t]."""
+        if self.training:
+            raise NotImplementedError("training-mode forward needs backward kernels (not provided)")
+        (I0, I1, x0, x1, sigma0, sigma1, dpt0, dpt1, inv_d0, inv_d1, m0, m1, poseI) = self._preprocess(
+            img0, img1, depth0, depth1, poseI=None, obj_mask0=obj_mask0, obj_mask1=obj_mask1)
+        pose = poseI
+        # the weight prior of level 3 (346) only feeds learned ICP scalers, which are not offered
+        for l in (3, 2, 1, 0):
+            out = getattr(self, f'tr_update{l}')(
+                pose, x0[l], x1[l], inv_d0[l], inv_d1[l], K / float(1 << l), sigma0=sigma0[l], sigma1=sigma1[l],
+                wPrior=None, vis_res=False, depth0=dpt0[l], depth1=dpt1[l], obj_mask0=m0[l], obj_mask1=m1[l])
+            pose = out[0]
+        return pose
+
+    def compute_residual(self, img0, img1, depth0, depth1, K, poseI=None, level_i=0, logger=None, vis=False,
+                         obj_mask0=None, obj_mask1=None):
+        """Residual-only loss at `level_i` for pose `poseI` (LeastSquareTracking.py:605-651)."""
+        (I0, I1, x0, x1, sigma0, sigma1, dpt0, dpt1, inv_d0, inv_d1, m0, m1, poseI) = self._preprocess(
+            img0, img1, depth0, depth1, poseI=poseI, obj_mask0=obj_mask0, obj_mask1=obj_mask1)
+        i = level_i
+        loss = self.tr_update0.forward_residuals(
+            poseI, x0[i], x1[i], inv_d0[i], inv_d1[i], K / float(1 << i), sigma0=sigma0[i], sigma1=sigma1[i],
+            wPrior=None, vis_res=False, depth0=dpt0[i], depth1=dpt1[i], obj_mask0=m0[i], obj_mask1=m1[i])
+        return poseI, loss
+
+    # ------------------------------------------------------------------ internals
+    def _encode(self, img0, invD0, img1, invD1):
+        if self.encoder_type == self.RGB:
+            B, _, H, W = img0.shape
+            grey = (img0[:, 0] * 0.299 + img0[:, 1] * 0.587 + img0[:, 2] * 0.114).view(B, 1, H, W)
+            x = self.construct_image_pyramids(grey)
+            return x, [torch.ones_like(a) for a in x], x
+        if self.encoder_type == self.CONV_RGBD:
+            return self.encoder(torch.cat((img0, invD0), dim=1))
+        return self.encoder(torch.cat((img0, invD0, img1, invD1), dim=1))
+
+    @staticmethod
+    def _inverse_depth(depth):
+        """clamp(1/depth, 0, 10) with the batch-global min and max zeroed (653-661)."""
+        invD = torch.clamp(1.0 / depth, 0, 10)
+        invD[invD == invD.min()] = 0
+        invD[invD == invD.max()] = 0
+        return invD
+
+    def _preprocess(self, img0, img1, depth0, depth1, poseI=None, obj_mask0=None, obj_mask1=None):
+        """LeastSquareTracking.py:653-699."""
+        invD0 = self._inverse_depth(depth0)
+        invD1 = self._inverse_depth(depth1)
+        I0 = color_normalize(img0)
+        I1 = color_normalize(img1)
+        with torch.no_grad():
+            x0, sigma0, orig_x0 = self._encode(I0, invD0, I1, invD1)
+            x1, sigma1, orig_x1 = self._encode(I1, invD1, I0, invD0)
+        inv_d0 = self.construct_depth_pyramids(invD0)
+        inv_d1 = self.construct_depth_pyramids(invD1)
+        if self.combine_icp:
+            dpt0 = self.construct_depth_pyramids(depth0)
+            dpt1 = self.construct_depth_pyramids(depth1)
+        else:
+            dpt0 = dpt1 = [None] * len(self.scales)
+        m0 = self.construct_image_pyramids(obj_mask0) if obj_mask0 is not None else [None] * len(self.scales)
+        m1 = self.construct_image_pyramids(obj_mask1) if obj_mask1 is not None else [None] * len(self.scales)
+        if poseI is None:
+            if self.predict_init_pose:
+                with torch.no_grad():
+                    R0, t0 = self.pose_predictor(orig_x0[3], orig_x1[3])
+            else:
+                B = invD0.shape[0]
+                R0 = torch.eye(3, dtype=torch.float).expand(B, 3, 3).type_as(I0)
+                t0 = torch.zeros(B, 3, 1, dtype=torch.float).type_as(I0)
+            poseI = [R0, t0]
+        return (I0, I1, x0, x1, sigma0, sigma1, dpt0, dpt1, inv_d0, inv_d1, m0, m1, poseI)

@@ -1,0 +1,380 @@
+"""Modules of the tracker: the HIP-backed U_IC solver and the host-side networks.
+
+`TrustRegionInverseWUncertainty` is the drop-in for the reference's class of the
+same name (code/models/algorithms.py:579-997): same constructor, same
+`forward` / `forward_residuals` signatures and return values, but every level
+runs through libdpft_ic.so (deep_prob_feature_track_amd.ic).  There is no
+PyTorch fallback: configurations the kernels do not implement raise
+NotImplementedError, CPU tensors raise RuntimeError.
+
+The networks around it (feature encoder, pose initialisers, estimator
+placeholders) are PyTorch modules whose parameter names match the reference's
+state_dict keys, so the reference's checkpoints load unchanged:
+  ImagePyramids 1201-1219, FeaturePyramid 1221-1430, DeepRobustEstimator
+  1432-1499, ScaleNet 1501-1581, DirectSolverNet 1583-1692 (structure; the
+  U_IC path never calls it, algorithms.py:691), PoseNetFeat / PoseNet /
+  SFMPoseNet 1694-1832, deep_damping_regressor 1834-1842.
+"""
+import torch
+import torch.nn as nn
+import torch.nn.functional as func
+
+from .. import ic
+from . import geometry
+from .submodules import convLayer as conv
+from .submodules import convLayer1d as conv1d
+from .submodules import fcLayer, initialize_weights
+
+
+# ------------------------------------------------------------------ pyramids
+class ImagePyramids(nn.Module):
+    """Average / max pooling by 2^s for every scale s; bool maps pool as float and
+    come back as `> 0` (algorithms.py:1201-1219)."""
+
+    def __init__(self, scales, pool='avg'):
+        super().__init__()
+        if pool not in ('avg', 'max'):
+            raise NotImplementedError(pool)
+        make = nn.AvgPool2d if pool == 'avg' else nn.MaxPool2d
+        self.multiscales = [make(1 << s, 1 << s) for s in scales]
+
+    def forward(self, x):
+        if x.dtype == torch.bool:
+            xf = x.to(torch.float32)
+            return [f(xf).to(torch.bool) for f in self.multiscales]
+        return [f(x) for f in self.multiscales]
+
+
+# ------------------------------------------------------------------ encoder
+_UNCERTAINTY_ACTIVATIONS = {
+    'gaussian': lambda s: torch.exp(0.5 * torch.clamp(s, min=-6, max=6)),
+    'laplacian': lambda s: torch.exp(torch.clamp(s, min=-3, max=3)),
+    'sigmoid': torch.sigmoid,
+    'old_gaussian': lambda s: torch.exp(0.5 * torch.clamp(s, min=1e-3, max=1e3)),
+    'old_laplacian': lambda s: torch.exp(torch.clamp(s, min=1e-3, max=1e3)),
+}
+
+
+class FeaturePyramid(nn.Module):
+    """Four-scale feature + uncertainty encoder (algorithms.py:1221-1430).
+
+    Returns (features [4], sigmas [4], backbone maps [4]); a 1-channel uncertainty
+    is repeated to the feature channels as in the reference (1426-1427) -- the
+    solver wrapper recognises the repeat and hands the kernel one plane."""
+
+    def __init__(self, D, w_uncertainty='None', feature_channel=1, feature_extract='conv', uncertainty_channel=1):
+        super().__init__()
+        assert uncertainty_channel == feature_channel or uncertainty_channel == 1
+        self.w_uncertainty = w_uncertainty != 'None'
+        self.uncertainty_type = w_uncertainty
+        self.output_C = feature_channel
+        self.uncertainty_C = uncertainty_channel
+        self.feature_extract = feature_extract
+        self.f_channels = [32, 64, 96, 128]
+        # backbone: per scale (in, mid, out) with dilations 1, 2, 2
+        stages = [(D, 16, 32, 32), (32, 32, 64, 64), (64, 64, 96, 96), (96, 96, 128, 128)]
+        for s, (cin, c1, c2, cout) in enumerate(stages):
+            net = nn.Sequential(conv(True, cin, c1, 3), conv(True, c1, c2, 3, dilation=2),
+                                conv(True, c2, cout, 3, dilation=2))
+            setattr(self, f'net{s}', net)
+            initialize_weights(net)
+
+        if feature_extract not in ('average', 'skip'):
+            if feature_extract == 'prob_fuse':
+                self.output_C = 16
+            if feature_extract in ('conv', 'prob_fuse'):
+                heads = [conv(True, c, self.output_C, kernel_size=1) for c in self.f_channels]
+            elif feature_extract == '1by1':
+                heads = [nn.Conv2d(c, self.output_C, kernel_size=(1, 1)) for c in self.f_channels]
+            else:
+                raise NotImplementedError("not supported feature extraction option")
+            for s, h in enumerate(heads):
+                setattr(self, f'f_conv{s}', h)
+            initialize_weights(heads)
+
+        if self.w_uncertainty and self.uncertainty_type != 'identity':
+            if self.uncertainty_type == 'feature':
+                heads = [conv(True, c, self.output_C, 1) for c in self.f_channels]
+            elif self.uncertainty_type in _UNCERTAINTY_ACTIVATIONS:
+                heads = [nn.Sequential(conv(True, c, 16, kernel_size=1), nn.Conv2d(16, self.uncertainty_C, kernel_size=1))
+                         for c in self.f_channels]
+            else:
+                raise NotImplementedError(self.uncertainty_type)
+            for s, h in enumerate(heads):
+                setattr(self, f'sigma_conv{s}', h)
+            initialize_weights(heads)
+
+        self.downsample = nn.AvgPool2d(kernel_size=2)
+
+    def _prob_fuse(self, x, head):
+        f, p = head(x).chunk(2, dim=1)
+        return torch.sum(f * torch.sigmoid(p), dim=1, keepdim=True)
+
+    def forward(self, x):
+        maps = []
+        for s in range(4):
+            x = getattr(self, f'net{s}')(x if s == 0 else self.downsample(x))
+            maps.append(x)
+
+        if self.feature_extract == 'skip':
+            f = list(maps)
+        elif self.feature_extract == 'average':
+            f = [m.sum(dim=1, keepdim=True) / m.shape[1] for m in maps]
+        elif self.feature_extract == 'prob_fuse':
+            f = [self._prob_fuse(m, getattr(self, f'f_conv{s}')) for s, m in enumerate(maps)]
+        elif self.feature_extract in ('conv', '1by1'):
+            f = [getattr(self, f'f_conv{s}')(m) for s, m in enumerate(maps)]
+        else:
+            raise NotImplementedError()
+
+        if not self.w_uncertainty:
+            return f, [None] * 4, maps
+        if self.uncertainty_type == 'identity':
+            return f, [torch.ones_like(fi) for fi in f], maps
+        sigma = [getattr(self, f'sigma_conv{s}')(m) for s, m in enumerate(maps)]
+        if self.uncertainty_type != 'feature':
+            sigma = [_UNCERTAINTY_ACTIVATIONS[self.uncertainty_type](si) for si in sigma]
+        if self.uncertainty_C == 1 and self.output_C != 1:
+            sigma = [si.repeat((1, self.output_C, 1, 1)) for si in sigma]
+        return f, sigma, maps
+
+
+# ------------------------------------------------------------------ estimator placeholders
+def _weight_net(D, final):
+    net = nn.Sequential(conv(True, D, 16, 3, dilation=1), conv(True, 16, 32, 3, dilation=2),
+                        conv(True, 32, 64, 3, dilation=4), *final)
+    initialize_weights(net)
+    return net
+
+
+class DeepRobustEstimator(nn.Module):
+    """M-estimator (algorithms.py:1432-1499).  The U_IC solver never applies it
+    (the call is commented out in the reference, algorithms.py:638-641); kept for
+    the constructor / state_dict surface."""
+
+    def __init__(self, estimator_type):
+        super().__init__()
+        if estimator_type == 'MultiScale2w':
+            self.D = 4
+            self.net = _weight_net(4, [conv(True, 64, 1, 3, dilation=1), nn.Sigmoid()])
+        elif estimator_type == 'None':
+            self.D = -1
+            self.net = None
+        else:
+            raise NotImplementedError()
+
+    def forward(self, residual, x0, x1, ws=None):
+        if self.D < 0:
+            return torch.ones_like(residual)
+        H, W = residual.shape[-2:]
+        wl = func.interpolate(ws, (H, W), mode='bilinear', align_corners=True)
+        return self.net(torch.cat((residual.abs(), x0, x1, wl), dim=1))
+
+
+class ScaleNet(nn.Module):
+    """ICP / feature balance (algorithms.py:1501-1581).  'None' is the constant
+    `scale` (0.01) the fused ICP kernel applies; the learned scalers need the
+    residual maps the kernel never materialises and are not offered."""
+
+    _DIMS = {'oneResidual': 1, 'twoResidual': 2, 'MultiScale2w': 3, 'expMultiScale': 3, 'None': -1}
+
+    def __init__(self, estimator_type, scale=None):
+        super().__init__()
+        if estimator_type not in self._DIMS:
+            raise NotImplementedError()
+        self.estimator_type = estimator_type
+        self.D = self._DIMS[estimator_type]
+        self.net = _weight_net(self.D, [conv(True, 64, 16, 3, dilation=1), nn.Conv2d(16, 1, kernel_size=1, padding=0)]) \
+            if self.D > 0 else None
+        self.scale = 0.01 if scale is None else scale
+
+    def forward(self, residual, another_residual=None, ws=None):
+        if self.D > 0:
+            raise NotImplementedError("learned ICP scalers are not supported by the fused HIP solver")
+        return torch.ones_like(residual) * self.scale
+
+
+def deep_damping_regressor(D):
+    """MLP D -> 128 -> 256 -> 6 with ReLUs (algorithms.py:1834-1842)."""
+    return nn.Sequential(fcLayer(D, 128), fcLayer(128, 256), fcLayer(256, 6))
+
+
+class DirectSolverNet(nn.Module):
+    """Damping module (algorithms.py:1583-1692).  The U_IC solver does not call it
+    (it always uses lev_mar_H, algorithms.py:836-846); kept for the surface and the
+    'Direct-ResVol' parameters."""
+
+    SOLVER_NO_DAMPING = 0
+    SOLVER_RESIDUAL_VOLUME = 1
+
+    def __init__(self, solver_type, samples=10, direction='inverse'):
+        super().__init__()
+        self.direction = direction
+        if solver_type == 'Direct-Nodamping':
+            self.net = None
+            self.type = self.SOLVER_NO_DAMPING
+        elif solver_type == 'Direct-ResVol':
+            self.samples = samples
+            self.net = deep_damping_regressor(D=6 * 6 + 6 * samples)
+            self.type = self.SOLVER_RESIDUAL_VOLUME
+            initialize_weights(self.net)
+        else:
+            raise NotImplementedError()
+
+    def forward(self, *args, **kwargs):
+        raise NotImplementedError("DirectSolverNet is not on the U_IC path (algorithms.py:691)")
+
+
+# ------------------------------------------------------------------ init-pose networks
+class PoseNetFeat(nn.Module):
+    """algorithms.py:1694-1720."""
+
+    def __init__(self):
+        super().__init__()
+        self.final_C = 1024
+        self.sep_cov = nn.Sequential(conv(True, 128, 128, kernel_size=3, stride=2),
+                                     conv(True, 128, 128, kernel_size=3, stride=2))
+        self.conv1 = conv1d(True, 128, 256, 1)
+        self.conv2 = conv1d(True, 256, 512, 1)
+        self.conv3 = conv1d(True, 512, self.final_C, 1)
+        initialize_weights((self.sep_cov, self.conv1, self.conv2, self.conv3))
+
+    def forward(self, feat_map):
+        B, C = feat_map.shape[:2]
+        emb1 = self.conv1(self.sep_cov(feat_map).view(B, C, -1))
+        emb2 = self.conv2(emb1)
+        final = self.conv3(emb2)
+        N = final.shape[-1]
+        pooled = func.avg_pool1d(final, N).view(B, self.final_C, 1).repeat(1, 1, N)
+        return emb1, emb2, pooled
+
+
+def _pose_head(cin, cout):
+    return nn.Sequential(conv1d(True, cin, 640, 1), conv1d(True, 640, 256, 1), conv1d(True, 256, 128, 1),
+                         nn.Conv1d(128, cout, kernel_size=1, padding=0))
+
+
+class PoseNet(nn.Module):
+    """Dense init-pose regressor (algorithms.py:1722-1768)."""
+
+    def __init__(self, scale_motion=0.01, multi_hypo='None', res_input=False):
+        super().__init__()
+        self.feat_net = PoseNetFeat()
+        self.input_C = 3584
+        self.scale_motion = scale_motion
+        self.net_r = _pose_head(self.input_C, 3)
+        self.net_t = _pose_head(self.input_C, 3)
+        self.net_c = _pose_head(self.input_C, 1)
+        initialize_weights((self.net_r, self.net_t, self.net_c))
+
+    def forward(self, x0, x1):
+        a = self.feat_net(x0)
+        b = self.feat_net(x1)
+        feat = torch.cat([a[0], b[0], a[1], b[1], a[2], b[2]], dim=1)
+        conf = func.softmax(self.net_c(feat), dim=-1)
+        rot = self.scale_motion * torch.sum(self.net_r(feat) * conf, dim=-1)
+        trs = self.scale_motion * torch.sum(self.net_t(feat) * conf, dim=-1)
+        return geometry.batch_euler2mat(rot[:, 0], rot[:, 1], rot[:, 2]), trs
+
+
+class SFMPoseNet(nn.Module):
+    """Init-pose regressor on the coarsest backbone maps (algorithms.py:1770-1832)."""
+
+    def __init__(self, scale_motion=0.01, multi_hypo='None', res_input=False):
+        super().__init__()
+        self.batchnorm = True
+        self.res_input = res_input
+        planes = [384, 256, 256] if res_input else [256, 256, 256]
+        self.scale_motion = scale_motion
+        self.multi_hypo = multi_hypo
+        self.hypo_num = 16 if multi_hypo != 'None' else 1
+        self.net = nn.Sequential(conv(True, planes[0], planes[1], kernel_size=3, dilation=2),
+                                 conv(True, planes[1], planes[2], kernel_size=3, dilation=2))
+        if multi_hypo == 'None':
+            self.final_layer = nn.Conv2d(planes[2], 6, kernel_size=1, padding=0)
+        elif multi_hypo in ('average', 'prob_fuse'):
+            per = 6 if multi_hypo == 'average' else 7
+            self.final_layer = nn.Sequential(conv1d(True, planes[2], 128, 1),
+                                             nn.Conv1d(128, self.hypo_num * per, kernel_size=1, padding=0))
+        else:
+            raise NotImplementedError(multi_hypo)
+        initialize_weights(self.net, self.final_layer)
+
+    def forward(self, x0, x1):
+        inp = torch.cat((x0, x1, x0 - x1) if self.res_input else (x0, x1), dim=1)
+        B = inp.shape[0]
+        h = self.net(inp)
+        if self.multi_hypo == 'None':
+            pose = self.final_layer(h).mean(dim=3).mean(dim=2)
+        else:
+            h = self.final_layer(h.view(B, h.shape[1], -1)).mean(dim=-1)
+            if self.multi_hypo == 'average':
+                pose = h.view(B, 6, -1).mean(dim=-1)
+            else:
+                poses, conf = h.view(B, -1, 7).split((6, 1), dim=-1)
+                pose = torch.sum(poses * func.softmax(conf, dim=1), dim=1)
+        return geometry.pose_vec2mat(self.scale_motion * pose.view(B, 6), rotation_mode='euler')
+
+
+# ------------------------------------------------------------------ the HIP-backed solver
+class TrustRegionInverseWUncertainty(nn.Module):
+    """Inverse-compositional, uncertainty-weighted Gauss-Newton with Levenberg
+    damping (algorithms.py:579-997), one level per call, on libdpft_ic.so.
+
+    forward  -> (pose [R, t], weights[, JtWJ])   algorithms.py:611-723
+    forward_residuals -> loss [B]                algorithms.py:725-786
+    `weights` is the reference's all-ones [B,C,H,W] map (a broadcast view, no
+    memory) or, with combine_icp, the constant ICP scale [B,1,H,W].
+    """
+
+    def __init__(self, max_iter=3, mEst_func=None, solver_func=None, timers=None, uncer_prop=False,
+                 combine_icp=False, scale_func=None, remove_tru_sigma=False):
+        super().__init__()
+        self.max_iterations = max_iter
+        self.mEstimator = mEst_func
+        self.directSolver = solver_func
+        self.timers = timers
+        self.uncer_prop = uncer_prop
+        self.combine_icp = combine_icp
+        self.scale_func = scale_func
+        self.remove_tru_sigma = remove_tru_sigma
+
+    def _check_path(self, x0):
+        if torch.is_grad_enabled() and x0.requires_grad:
+            raise NotImplementedError("the HIP U_IC solver is inference-only (no backward kernels)")
+        if self.combine_icp and self.scale_func is not None and getattr(self.scale_func, 'D', -1) > 0:
+            raise NotImplementedError("learned ICP scalers are not supported by the fused HIP solver")
+
+    def _icp_scale(self):
+        return float(self.scale_func.scale) if self.scale_func is not None else 0.01
+
+    def _common(self, x0, depth0, depth1, obj_mask0, obj_mask1):
+        kw = dict(remove_tru_sigma=bool(self.remove_tru_sigma), obj_mask0=obj_mask0, obj_mask1=obj_mask1)
+        if self.combine_icp:
+            assert depth0 is not None and depth1 is not None
+            kw.update(combine_icp=True, depth0=depth0, depth1=depth1, icp_weight=self._icp_scale())
+        return kw
+
+    def forward(self, pose10, x0, x1, invD0, invD1, K, sigma0, sigma1, wPrior=None,
+                depth0=None, depth1=None, vis_res=True, obj_mask0=None, obj_mask1=None):
+        assert sigma0 is not None and sigma1 is not None
+        self._check_path(x0)
+        B, C, H, W = x0.shape
+        kw = self._common(x0, depth0, depth1, obj_mask0, obj_mask1)
+        with torch.no_grad():
+            out = ic.solve_level(pose10, x0, x1, invD0, invD1, K, sigma0, sigma1, iters=self.max_iterations,
+                                 return_jtj=self.uncer_prop, **kw)
+        pose = [out[0], out[1]]
+        if self.combine_icp:
+            weights = torch.full((1, 1, 1, 1), self._icp_scale(), dtype=x0.dtype, device=x0.device).expand(B, 1, H, W)
+        else:
+            weights = torch.ones((1, 1, 1, 1), dtype=x0.dtype, device=x0.device).expand(B, C, H, W)
+        return (pose, weights, out[2]) if self.uncer_prop else (pose, weights)
+
+    def forward_residuals(self, pose10, x0, x1, invD0, invD1, K, sigma0, sigma1, wPrior=None,
+                          depth0=None, depth1=None, vis_res=True, obj_mask0=None, obj_mask1=None):
+        assert sigma0 is not None and sigma1 is not None
+        self._check_path(x0)
+        kw = self._common(x0, depth0, depth1, obj_mask0, obj_mask1)
+        with torch.no_grad():
+            return ic.residual_level(pose10, x0, x1, invD0, invD1, K, sigma0, sigma1, **kw)

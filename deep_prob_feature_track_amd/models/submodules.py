@@ -1,0 +1,64 @@
+"""Network building blocks of the tracker's host-side modules.
+
+Restates the reference's code/models/submodules.py (color_normalize 20-23,
+convLayer 25-39, convLayer1d 41-55, fcLayer 57-61, initialize_weights 63-78)
+so that modules built from them carry the reference's state_dict keys:
+a block is nn.Sequential(conv[, batchnorm], ELU) -> keys `<name>.0.weight`,
+`<name>.1.running_mean`, ...
+"""
+import torch
+import torch.nn as nn
+from torch.nn import init
+
+_RGB_MEAN = (0.4914, 0.4822, 0.4465)
+_RGB_STD = (0.2023, 0.1994, 0.2010)
+
+
+def color_normalize(color):
+    """Per-channel (x - mean) / std of an RGB batch [B,3,H,W] (submodules.py:20-23)."""
+    mean = torch.tensor(_RGB_MEAN, dtype=color.dtype, device=color.device).view(1, 3, 1, 1)
+    std = torch.tensor(_RGB_STD, dtype=color.dtype, device=color.device).view(1, 3, 1, 1)
+    return (color - mean) / std
+
+
+def _padding(kernel_size, dilation):
+    # the reference's "same" padding formula (kept literally: it is not k//2*d for every d)
+    return (kernel_size - 1) // 2 + dilation - 1
+
+
+def _block(conv_cls, bn_cls, batch_norm, cin, cout, kernel_size, stride, dilation, bias):
+    layers = [conv_cls(cin, cout, kernel_size=kernel_size, stride=stride,
+                       padding=_padding(kernel_size, dilation), dilation=dilation,
+                       bias=bias if batch_norm else True)]
+    if batch_norm:
+        layers.append(bn_cls(cout))
+    layers.append(nn.ELU(inplace=True))
+    return nn.Sequential(*layers)
+
+
+def convLayer(batchNorm, in_planes, out_planes, kernel_size=3, stride=1, dilation=1, bias=False):
+    """Conv2d [+ BatchNorm2d] + ELU."""
+    return _block(nn.Conv2d, nn.BatchNorm2d, batchNorm, in_planes, out_planes, kernel_size, stride, dilation, bias)
+
+
+def convLayer1d(batchNorm, in_planes, out_planes, kernel_size=3, stride=1, dilation=1, bias=False):
+    """Conv1d [+ BatchNorm1d] + ELU."""
+    return _block(nn.Conv1d, nn.BatchNorm1d, batchNorm, in_planes, out_planes, kernel_size, stride, dilation, bias)
+
+
+def fcLayer(in_planes, out_planes, bias=True):
+    """Linear + ReLU."""
+    return nn.Sequential(nn.Linear(in_planes, out_planes, bias), nn.ReLU(inplace=True))
+
+
+def initialize_weights(modules, method='xavier'):
+    """Xavier / Kaiming-uniform init of the Conv2d / ConvTranspose2d among `modules`
+    (their direct iteration, as the reference does), zero biases."""
+    for m in modules:
+        if isinstance(m, (nn.Conv2d, nn.ConvTranspose2d)):
+            if m.bias is not None:
+                m.bias.data.zero_()
+            if method == 'xavier':
+                init.xavier_uniform_(m.weight)
+            elif method == 'kaiming':
+                init.kaiming_uniform_(m.weight)

@@ -69,6 +69,44 @@ def depth_m(idx, base_down=1):
     return np.clip(d, np.float32(0.5), np.float32(5.0)).astype(np.float32)
 
 
+def color_float(idx, base_down=1):
+    """[3, H, W] RGB in [0, 1] (nearest subsampling; uint8 / 255 in fp32)."""
+    color, _ = frames()
+    c = color[idx][::base_down, ::base_down].astype(np.float32)
+    return (np.moveaxis(c, -1, 0) / np.float32(255.0)).astype(np.float32)
+
+
+def synthetic_weights(key, shape, gain=1.5):
+    """Deterministic stand-in for trained weights (the checkpoints are absent).
+
+    Conv / linear weights: hashed-integer uniform values with variance
+    gain^2 / fan_in; biases 0; BatchNorm at identity statistics.  Integer mixing
+    and exactly-rounded float32 ops only, so every host produces the same bits."""
+    shape = tuple(int(v) for v in shape)
+    leaf = key.rsplit(".", 1)[-1]
+    if leaf == "num_batches_tracked":
+        return np.zeros(shape, np.int64)
+    if leaf in ("running_mean", "bias"):
+        return np.zeros(shape, np.float32)
+    if leaf == "running_var":
+        return np.ones(shape, np.float32)
+    if len(shape) == 1:  # BatchNorm weight
+        return np.ones(shape, np.float32)
+    if "sigma_conv" in key:  # keep the uncertainty heads off their clamps
+        gain = 0.1
+    n = int(np.prod(shape))
+    fan_in = n // shape[0]
+    seed = np.uint64(sum((k + 1) * ord(ch) for k, ch in enumerate(key)))
+    h = np.arange(n, dtype=np.uint64) * np.uint64(2654435761) + seed * np.uint64(40503)
+    h &= np.uint64(0xFFFFFFFF)
+    for sh in (16, 13, 16):  # integer avalanche mix (exact, host-independent)
+        h ^= h >> np.uint64(sh)
+        h = (h * np.uint64(0x45D9F3B)) & np.uint64(0xFFFFFFFF)
+    u = (h >> np.uint64(8)).astype(np.float32) / np.float32(16777216.0) - np.float32(0.5)  # [-0.5, 0.5)
+    scale = np.float32(gain * np.sqrt(12.0 / fan_in))
+    return (u * scale).astype(np.float32).reshape(shape)
+
+
 def features(idx, C, level, base_down=1):
     """[C, H_l, W_l] feature stack and [1, H_l, W_l] sigma for frame idx at level."""
     g, npx = grey_int(idx, base_down)

@@ -1,0 +1,35 @@
+"""The C-ABI library loads (no GPU needed) and exports every entry point include/dpft_ic.h declares."""
+import os
+import re
+
+from deep_prob_feature_track_amd import _native as N
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def declared_functions():
+    src = open(os.path.join(ROOT, "include", "dpft_ic.h")).read()
+    src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
+    return sorted(set(re.findall(r"\b(dpft_[a-z_]+)\s*\(", src)))
+
+
+def test_header_declares_the_binding_surface():
+    assert declared_functions() == sorted(N.EXPORTS)
+
+
+def test_library_exports_every_declared_symbol():
+    L = N.lib()
+    for name in declared_functions():
+        assert hasattr(L, name), name
+    assert L.dpft_version() == N.ABI_VERSION
+
+
+def test_invalid_descriptor_is_rejected_without_device_work():
+    import ctypes
+    L = N.lib()
+    bad = N.LevelDesc(0, 8, 1, 120, 160, 3, 0, 0.0)
+    assert L.dpft_workspace_size(ctypes.byref(bad)) == 0
+    rc = L.dpft_ic_solve_level(ctypes.byref(bad), None, None, None, None, None, None, 0, None)
+    assert rc == -1 and b"bad shape" in L.dpft_last_error()
+    cs = N.LevelDesc(1, 8, 3, 120, 160, 3, 0, 0.0)  # Cs must be 1 or C
+    assert L.dpft_workspace_size(ctypes.byref(cs)) == 0

@@ -1,0 +1,100 @@
+"""Drop-in `models.LeastSquareTracking` against the reference's own module outputs.
+
+Fixtures: tests/golden/gen_model_golden.py ran the REFERENCE LeastSquareTracking
+(CPU fp32, deterministic synthetic weights from recipe.synthetic_weights) and
+stored its state_dict keys / shapes, forward() poses and compute_residual()
+losses.  Here the build's mirror is constructed with the same arguments, loaded
+with the same weights, and run on the GPU (encoder in PyTorch, solver in HIP).
+"""
+import json
+import os
+
+import numpy as np
+import pytest
+import torch
+
+import recipe
+import gen_model_golden as G
+from deep_prob_feature_track_amd.models.LeastSquareTracking import LeastSquareTracking, default_options
+
+HERE = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
+KEYS = json.load(open(os.path.join(HERE, "model_keys.json")))
+
+
+def build(spec, mest="None", solver="Direct-Nodamping", no_weight_sharing=False):
+    return LeastSquareTracking(spec["encoder"], spec["uncertainty"], 3, mest, solver,
+                               options=default_options(**spec["opts"]), no_weight_sharing=no_weight_sharing)
+
+
+@pytest.mark.parametrize("name", sorted(G.KEY_VARIANTS))
+def test_state_dict_surface_variants(name):
+    spec = G.KEY_VARIANTS[name]
+    m = build(spec, spec["mest"], spec["solver"], spec["no_weight_sharing"])
+    got = [[k, list(v.shape)] for k, v in m.state_dict().items()]
+    assert got == KEYS[name]
+
+
+@pytest.mark.parametrize("name", sorted(G.MODEL_CASES))
+def test_state_dict_surface_cases(name):
+    m = build(G.MODEL_CASES[name])
+    got = [[k, list(v.shape)] for k, v in m.state_dict().items()]
+    assert got == KEYS[name]
+    z = np.load(os.path.join(HERE, f"model_{name}.npz"), allow_pickle=False)
+    assert list(z["keys"]) == [k for k, _ in got]
+
+
+def test_unsupported_tracker_types_raise():
+    spec = G.MODEL_CASES["convrgbd2_c8"]
+    with pytest.raises(NotImplementedError):
+        LeastSquareTracking(spec["encoder"], "None", 3, "None", "Direct-Nodamping",
+                            options=default_options(**spec["opts"]))  # IC tracker
+    with pytest.raises(NotImplementedError):
+        LeastSquareTracking(spec["encoder"], "laplacian", 3, "None", "Direct-Nodamping", direction="forward",
+                            options=default_options(**spec["opts"]))  # U_FC tracker
+
+
+def _loaded(name, device):
+    spec = G.MODEL_CASES[name]
+    m = build(spec)
+    m.load_state_dict({k: torch.from_numpy(recipe.synthetic_weights(k, v.shape)) for k, v in m.state_dict().items()})
+    m.eval()
+    inp = G.model_inputs(spec["pairs"], spec["masks"])
+    T = {k: torch.from_numpy(v).to(device) for k, v in inp.items()}
+    return m.to(device), T
+
+
+def test_cpu_tensors_have_no_fallback():
+    m, T = _loaded("rgb_identity_masks", "cpu")
+    with pytest.raises(RuntimeError, match="no CPU fallback"):
+        m(T["img0"], T["img1"], T["depth0"], T["depth1"], T["K"])
+
+
+def test_training_mode_forward_raises():
+    m, T = _loaded("rgb_identity_masks", "cpu")
+    m.train()
+    with pytest.raises(NotImplementedError):
+        m(T["img0"], T["img1"], T["depth0"], T["depth1"], T["K"])
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("name", sorted(G.MODEL_CASES))
+def test_forward_and_residual_match_reference(name):
+    m, T = _loaded(name, "cuda")
+    z = np.load(os.path.join(HERE, f"model_{name}.npz"), allow_pickle=False)
+    kw = dict(obj_mask0=T.get("mask0"), obj_mask1=T.get("mask1"))
+    with torch.no_grad():
+        R, t = m(T["img0"], T["img1"], T["depth0"], T["depth1"], T["K"], **kw)
+        B = R.shape[0]
+        # se(3) tolerance of the contract: 1e-4; the encoder runs on MIOpen here
+        # and on the CPU in the reference, so features differ in the last bits.
+        assert np.abs(R.cpu().numpy() - z["R"]).max() < 1e-4
+        assert np.abs(t.cpu().numpy().reshape(B, 3) - z["t"].reshape(B, 3)).max() < 1e-4
+        Rr = torch.from_numpy(z["R"]).cuda()
+        tr = torch.from_numpy(z["t"]).cuda()
+        _, loss = m.compute_residual(T["img0"], T["img1"], T["depth0"], T["depth1"], T["K"], poseI=[Rr, tr],
+                                     level_i=0, **kw)
+        np.testing.assert_allclose(loss.cpu().numpy(), z["res_pose_loss"], rtol=1e-4)
+        ident = [torch.eye(3, device="cuda").expand(B, 3, 3).contiguous(), torch.zeros(B, 3, 1, device="cuda")]
+        _, loss2 = m.compute_residual(T["img0"], T["img1"], T["depth0"], T["depth1"], T["K"], poseI=ident,
+                                      level_i=2, **kw)
+        np.testing.assert_allclose(loss2.cpu().numpy(), z["res_init_loss"], rtol=1e-4)
