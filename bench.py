@@ -105,7 +105,7 @@ def main():
         dist.init_process_group("nccl")
     device = torch.device("cuda", local)
     torch.cuda.set_device(device)
-    from deep_prob_feature_track_amd import ic
+    from deep_prob_feature_track_amd import ic, shard
 
     B = a.batch_per_gpu
     sel, levels, K = make_inputs(B, rank, device)
@@ -143,8 +143,7 @@ def main():
         else:
             solve()
         if world > 1:
-            import torch.distributed as dist
-            dist.all_gather_into_tensor(gathered, torch.cat((R.view(B, 9), t), 1))
+            shard.gather_poses(R, t, out=gathered)
 
     def barrier():
         if world > 1:

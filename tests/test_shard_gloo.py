@@ -1,0 +1,93 @@
+"""Multi-process path on CPU: world_size-2 gloo run of the pair-sharded solve.
+
+Each rank solves its contiguous shard of a 4-pair batch (the oracle stands in for
+the GPU solver -- test infrastructure only) and all-gathers the poses with
+`shard.gather_poses`, the same call bench.py makes over RCCL.  Rank 0 checks the
+gathered tensor against per-shard solves done locally (shard semantics: the
+batch-global truncated-sigma extrema are per shard, as under the reference's
+nn.DataParallel).
+"""
+import os
+import socket
+
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+from deep_prob_feature_track_amd import shard
+
+PAIRS = [(0, 1), (1, 2), (2, 3), (3, 4)]
+
+
+def test_shard_range_partitions():
+    for n in (1, 4, 7, 64):
+        for world in (1, 2, 3, 8):
+            spans = [shard.shard_range(n, world, r) for r in range(world)]
+            assert spans[0][0] == 0 and spans[-1][1] == n
+            assert all(a[1] == b[0] for a, b in zip(spans, spans[1:]))
+            sizes = [e - b for b, e in spans]
+            assert max(sizes) - min(sizes) <= 1
+    with pytest.raises(ValueError):
+        shard.shard_range(4, 2, 2)
+
+
+def test_pack_unpack_roundtrip():
+    R = torch.randn(3, 3, 3)
+    t = torch.randn(3, 3, 1)
+    R2, t2 = shard.unpack_poses(shard.pack_poses(R, t))
+    assert torch.equal(R2, R) and torch.equal(t2, t)
+
+
+def _solve_pairs(pairs):
+    import golden_io
+    import recipe
+    from oracle import ic_oracle as O
+    case = recipe.make_case(pairs=pairs, C=8, levels=1, base_down=4)
+    level = golden_io.levels_torch(case, torch.float32)[0]
+    R0, t0 = golden_io.init_pose(case, torch.float32)
+    K = torch.from_numpy(case["K"])
+    with torch.no_grad():
+        return O.solve_pyramid(R0, t0, [level], K, iters=3, remove_tru_sigma=True)
+
+
+def _worker(rank, world, port, q, paths):
+    import sys
+    sys.path[:0] = paths
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    torch.set_num_threads(2)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        b, e = shard.shard_range(len(PAIRS), world, rank)
+        R, t = _solve_pairs(PAIRS[b:e])
+        out = shard.gather_poses(R, t)
+        if rank == 0:
+            q.put(out.clone())
+    finally:
+        dist.destroy_process_group()
+
+
+def _free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def test_two_rank_gloo_gather_matches_per_shard_solves():
+    world = 2
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    import sys
+    procs = [ctx.Process(target=_worker, args=(r, world, port, q, list(sys.path))) for r in range(world)]
+    for p in procs:
+        p.start()
+    gathered = q.get(timeout=120)
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    expect = []
+    for r in range(world):
+        b, e = shard.shard_range(len(PAIRS), world, r)
+        expect.append(shard.pack_poses(*_solve_pairs(PAIRS[b:e])))
+    assert torch.equal(gathered, torch.cat(expect, 0))
