@@ -99,7 +99,8 @@ constexpr int L_SUM = 0, L_NINV = 1, L_MN_ALL = 2, L_MN0 = 3, L_LMN = 4, L_NMN =
 // the two "blocks done" counters of the last-block finalizers, and the per-block
 // partial extrema of the sigma0 pass.  The counters are zero between calls: the
 // caller zero-fills the workspace once, every last block resets its counter.
-constexpr int kCtlMin = 0, kCtlMax = 1, kCtlDone = 2, kCtlMMDone = 3, kCtlResDone = 4, kCtlPart = 64, kCtlPair = 1152;
+constexpr int kCtlMin = 0, kCtlMax = 1, kCtlDone = 2, kCtlMMDone = 3, kCtlResDone = 4, kCtlD1Min = 8,
+              kCtlPart = 64, kCtlPair = 1152;
 constexpr int kMaxMMBlocks = 512;
 constexpr int kMaxPairs = 2048;  // per call (one completion counter per pair)
 constexpr int kMaxGrid = 4096;   // reduce-kernel workgroups (resident capacity is far below)
@@ -186,7 +187,8 @@ struct Taps {
 // geometry.py:359-364 normalises u,v to [-1,1]; grid_sample(align_corners=True,
 // padding_mode='border') maps back with (g + 1) * (size - 1) / 2, clamps to
 // [0, size-1], and weighs the four neighbours by products of the distances.
-__device__ __forceinline__ Taps make_taps(float u, float v, int H, int W) {
+__device__ __forceinline__ Taps make_taps_xy(float u, float v, int H, int W, int& tx0, int& tx1, int& ty0,
+                                             int& ty1) {
 #pragma clang fp contract(off)
   const float sx = (float)(W - 1) * 0.5f;
   const float sy = (float)(H - 1) * 0.5f;
@@ -212,7 +214,15 @@ __device__ __forceinline__ Taps make_taps(float u, float v, int H, int W) {
   t.ne = s * w;
   t.sw = n * e;
   t.se = n * w;
+  tx0 = x0;
+  tx1 = x1;
+  ty0 = y0;
+  ty1 = y1;
   return t;
+}
+__device__ __forceinline__ Taps make_taps(float u, float v, int H, int W) {
+  int a, b, c, d;
+  return make_taps_xy(u, v, H, W, a, b, c, d);
 }
 
 // An out-of-range neighbour always has weight exactly 0 under border clamping,
@@ -281,6 +291,10 @@ struct IterParams {
   const float* invD1;
   const uint8_t* mask0;
   const uint8_t* mask1;
+  const float* depth0;   // COMBINE_ICP: raw depth pyramids level (max-pooled), [B,1,H,W]
+  const float* depth1;
+  const float* nrm1;     // COMBINE_ICP: normal map of frame 1, [B,3,H,W] (workspace, per level)
+  float icp_w;           // ScaleNet('None') weight (algorithms.py:1563)
   const float* K;
   const float* R;
   const float* t;
@@ -468,6 +482,104 @@ struct ChanLoads {
   float t, m, b;  // f0 column in rows y-1, y, y+1
   Gather4 g;      // f1 taps
 };
+
+// ============================================================ ICP term (combine_ICP)
+// Point-to-plane residual and inverse Jacobian of one pixel, ScaleNet('None')
+// weight applied (algorithms.py:916-997, 668-689; geometry.py:1129-1136).
+// Frame 1's normal map is pose-independent and comes from icp_normals_kernel.
+struct IcpTerm {
+  float J[6];  // w * J (already the reference's negated, sigma-normalised J)
+  float r;     // w * r (1e-6 * w where occluded)
+  bool occ;
+};
+
+__device__ __forceinline__ IcpTerm icp_pixel(float xr, float yr, float d0, const float* __restrict__ Rm,
+                                             const float* __restrict__ tv, float fx, float fy, float cx, float cy,
+                                             int H, int W, const float* __restrict__ dep1,
+                                             const float* __restrict__ nrm1, int HW, bool mask0_bg,
+                                             const uint8_t* __restrict__ m1b, float wgt) {
+#pragma clang fp contract(off)
+  // vertex0 = [px, py, 1] * depth0; P = R V0 + t (CPU bmm order, then + t)
+  const float V0x = xr * d0, V0y = yr * d0, V0z = d0;
+  const float Px = __builtin_fmaf(Rm[2], V0z, __builtin_fmaf(Rm[1], V0y, Rm[0] * V0x)) + tv[0];
+  const float Py = __builtin_fmaf(Rm[5], V0z, __builtin_fmaf(Rm[4], V0y, Rm[3] * V0x)) + tv[1];
+  const float Pz = __builtin_fmaf(Rm[8], V0z, __builtin_fmaf(Rm[7], V0y, Rm[6] * V0x)) + tv[2];
+  const float u = (Px / Pz) * fx + cx;
+  const float v = (Py / Pz) * fy + cy;
+  const bool inview = (u > 0.0f) && (u < (float)(W - 1)) && (v > 0.0f) && (v < (float)(H - 1));
+  int x0, x1, y0, y1;
+  const Taps tp = make_taps_xy(u, v, H, W, x0, x1, y0, y1);
+  // vertex1 sampled: the vertex map at the four taps, then the sampler's chain
+  const float a = dep1[tp.o00], b = dep1[tp.o01], c = dep1[tp.o10], d = dep1[tp.o11];
+  const float px0 = ((float)x0 - cx) / fx, px1 = ((float)x1 - cx) / fx;
+  const float py0 = ((float)y0 - cy) / fy, py1 = ((float)y1 - cy) / fy;
+  const float V1x = bil4(px0 * a, px1 * b, px0 * c, px1 * d, tp);
+  const float V1y = bil4(py0 * a, py0 * b, py1 * c, py1 * d, tp);
+  const float V1z = bil4(a, b, c, d, tp);
+  const float Nx = bil(nrm1, tp), Ny = bil(nrm1 + HW, tp), Nz = bil(nrm1 + 2 * HW, tp);
+  const float Dx = Px - V1x, Dy = Py - V1y, Dz = Pz - V1z;
+  bool occ = !inview || (sqrtf((Dx * Dx + Dy * Dy) + Dz * Dz) > 0.1f) || mask0_bg;
+  if (m1b) occ = occ || !(bil_u8(m1b, tp) > 0.0f);
+  float r = (Nx * Dx + Ny * Dy) + Nz * Dz;
+  // n = N1w^T R ; J = [n x V0, -n]
+  const float n0 = __builtin_fmaf(Nz, Rm[6], __builtin_fmaf(Ny, Rm[3], Nx * Rm[0]));
+  const float n1 = __builtin_fmaf(Nz, Rm[7], __builtin_fmaf(Ny, Rm[4], Nx * Rm[1]));
+  const float n2 = __builtin_fmaf(Nz, Rm[8], __builtin_fmaf(Ny, Rm[5], Nx * Rm[2]));
+  // stereo-model sigma with the reference's hard-coded TUM constants (975-997)
+  const float sxy = d0 / 525.0f * 5.5f;
+  const float sz = d0 * d0 * 0.4f / (525.0f * 1.2f);
+  const float cov = (((n0 * sxy) * sxy) * n0 + ((n1 * sxy) * sxy) * n1) + ((n2 * sz) * sz) * n2;
+  const float sig = sqrtf(cov + 1e-8f) + 1e-8f;
+  IcpTerm o;
+  o.J[0] = -((n1 * V0z - n2 * V0y) / sig) * wgt;
+  o.J[1] = -((n2 * V0x - n0 * V0z) / sig) * wgt;
+  o.J[2] = -((n0 * V0y - n1 * V0x) / sig) * wgt;
+  o.J[3] = -((-n0) / sig) * wgt;
+  o.J[4] = -((-n1) / sig) * wgt;
+  o.J[5] = -((-n2) / sig) * wgt;
+  r = r / sig;
+  o.r = (occ ? 1e-6f : r) * wgt;
+  o.occ = occ;
+  return o;
+}
+
+// Frame-1 normal map of one level (algorithms.py:2148-2172): vertex map
+// (geometry.py:1129-1136), unnormalised replicate-padded Sobel, cross product,
+// / (|n| + 1e-8), zero where depth equals the batch-global min or max.
+__global__ __launch_bounds__(kThreads) void icp_normals_kernel(const float* __restrict__ depth, const float* __restrict__ K,
+                                                               int B, int H, int W, const uint32_t* __restrict__ dext,
+                                                               float* __restrict__ nrm) {
+  const int HW = H * W;
+  const long i = (long)blockIdx.x * kThreads + threadIdx.x;
+  if (i >= (long)B * HW) return;
+  const int b = (int)(i / HW), pix = (int)(i - (long)b * HW), y = pix / W, x = pix - y * W;
+  const float fx = K[4 * b + 0], fy = K[4 * b + 1], cx = K[4 * b + 2], cy = K[4 * b + 3];
+  const float* db = depth + (size_t)b * HW;
+  float V[3][3][3];  // [dy][dx][xyz]
+#pragma unroll
+  for (int j = 0; j < 3; ++j)
+#pragma unroll
+    for (int k = 0; k < 3; ++k) {
+      const int yy = min(max(y + j - 1, 0), H - 1), xx = min(max(x + k - 1, 0), W - 1);
+      const float dd = db[yy * W + xx];
+      V[j][k][0] = (((float)xx - cx) / fx) * dd;
+      V[j][k][1] = (((float)yy - cy) / fy) * dd;
+      V[j][k][2] = dd;
+    }
+  float gx[3], gy[3];
+#pragma unroll
+  for (int c = 0; c < 3; ++c) {
+    gx[c] = ((V[0][2][c] - V[0][0][c]) + 2.0f * (V[1][2][c] - V[1][0][c])) + (V[2][2][c] - V[2][0][c]);
+    gy[c] = ((V[2][0][c] - V[0][0][c]) + 2.0f * (V[2][1][c] - V[0][1][c])) + (V[2][2][c] - V[0][2][c]);
+  }
+  float n[3] = {gx[1] * gy[2] - gx[2] * gy[1], gx[2] * gy[0] - gx[0] * gy[2], gx[0] * gy[1] - gx[1] * gy[0]};
+  const float mag = sqrtf((n[0] * n[0] + n[1] * n[1]) + n[2] * n[2]) + 1e-8f;
+  const float d = db[pix];
+  const bool bad = d == dec_ord(dext[0]) || d == dec_ord(dext[1]);
+  float* o = nrm + (size_t)b * 3 * HW + pix;
+#pragma unroll
+  for (int c = 0; c < 3; ++c) o[(size_t)c * HW] = bad ? 0.0f : n[c] / mag;
+}
 
 // ============================================================ last-block finalize
 __device__ __forceinline__ double wave_sum_d(double v) {
@@ -774,7 +886,7 @@ __device__ void finalize_loss(const FinParams& q) {
 // prologue / epilogue per workgroup, and consecutive tiles are vertically
 // adjacent, so the halo rows of f0 / sigma0 are re-read from L2 right after
 // their first use.  Workgroup k writes record slot k.
-template <int CT, bool CS1, bool TRU>
+template <int CT, bool CS1, bool TRU, bool ICP>
 __global__ __launch_bounds__(kThreads, DPFT_MIN_WAVES) void ic_reduce_kernel(IterParams p) {
   const int C = CT > 0 ? CT : p.C;
   __shared__ float lds_ext[TRU ? 2 * 7 : 1][kThreads];  // extremum corrections (6 + count), min then max
@@ -985,6 +1097,19 @@ __global__ __launch_bounds__(kThreads, DPFT_MIN_WAVES) void ic_reduce_kernel(Ite
 #pragma unroll
       for (int i = 0; i < 6; ++i) acc[21 + i] -= cA * Jx[i] + cB * Jy[i];
       ninv += invalid ? 1.0f : 0.0f;
+      if (ICP) {  // JtWJ += (wJ)^T (wJ), JtR += (wJ)^T (w r)  (algorithms.py:668-689)
+        const float d0v = p.depth0[(size_t)b * HW + y * W + xc];
+        const IcpTerm ic = icp_pixel(wp.xr, wp.yr, d0v, Rm, tv, fx, fy, cx, cy, H, W, p.depth1 + (size_t)b * HW,
+                                     p.nrm1 + (size_t)b * 3 * HW, HW, !m0, m1b, p.icp_w);
+        int kq2 = 0;
+#pragma unroll
+        for (int i = 0; i < 6; ++i) {
+#pragma unroll
+          for (int j = i; j < 6; ++j) acc[kq2++] += ic.J[i] * ic.J[j];
+        }
+#pragma unroll
+        for (int i = 0; i < 6; ++i) acc[21 + i] += ic.J[i] * ic.r;
+      }
 
       if (TRU) {
         mn_all = fminf(mn_all, srmin);
@@ -1091,7 +1216,7 @@ __global__ __launch_bounds__(kThreads, DPFT_MIN_WAVES) void ic_reduce_kernel(Ite
 }
 
 // ============================================================ residual-only kernel
-template <bool CS1>
+template <bool CS1, bool ICP>
 __global__ __launch_bounds__(kThreads) void ic_residual_kernel(IterParams p) {
   __shared__ float red[4][16];
   const int tid = threadIdx.x, lane = tid & 63, wave = wave_id();
@@ -1138,6 +1263,13 @@ __global__ __launch_bounds__(kThreads) void ic_residual_kernel(IterParams p) {
     }
     bool inv = px.invalid;
     if (tru) inv = inv || (s00 == g0min) || (s00 == g0max);
+    if (ICP) {  // forward_residuals: ICP without object masks, combined occlusion (algorithms.py:765-782)
+      const IcpTerm ic = icp_pixel(px.xr, px.yr, p.depth0[(size_t)b * HW + pix], Rm, tv, fx, fy, cx, cy, H, W,
+                                   p.depth1 + (size_t)b * HW, p.nrm1 + (size_t)b * 3 * HW, HW, false, nullptr,
+                                   p.icp_w);
+      inv = inv || ic.occ;
+      srr = srr + ic.r * ic.r;
+    }
     sum += inv ? 0.f : srr;
     ninv += inv ? 1.f : 0.f;
     if (tru) {
@@ -1215,7 +1347,8 @@ __global__ __launch_bounds__(kThreads) void ic_debug_pixels_kernel(IterParams p,
 
 // sigma0 batch-global min / max (algorithms.py:1976-1977).  Per-workgroup
 // partials, the last workgroup reduces them in a fixed order (no atomics on data).
-__global__ __launch_bounds__(kThreads) void minmax_kernel(const float* __restrict__ s, size_t n, uint32_t* ctrl) {
+__global__ __launch_bounds__(kThreads) void minmax_kernel(const float* __restrict__ s, size_t n, uint32_t* ctrl,
+                                                          int slot) {
   __shared__ float sm[2][4];
   float mn = INFINITY, mx = -INFINITY;
   const size_t stride = (size_t)gridDim.x * kThreads;
@@ -1252,8 +1385,8 @@ __global__ __launch_bounds__(kThreads) void minmax_kernel(const float* __restric
       mx = fmaxf(mx, __shfl_xor(mx, off));
     }
     if (threadIdx.x == 0) {
-      ctrl[kCtlMin] = enc_ord(mn);
-      ctrl[kCtlMax] = enc_ord(mx);
+      ctrl[slot] = enc_ord(mn);
+      ctrl[slot + 1] = enc_ord(mx);
     }
   }
 }
@@ -1284,13 +1417,16 @@ int check_desc(const DpftLevelDesc* d) {
   if (d->Cs != 1 && d->Cs != d->C) return fail(DPFT_E_INVALID, "Cs must be 1 or C (got %d, C=%d)", d->Cs, d->C);
   if ((long)d->H * d->W >= (1L << 30)) return fail(DPFT_E_INVALID, "level too large");
   if (d->B > kMaxPairs) return fail(DPFT_E_INVALID, "B=%d exceeds %d pairs per call", d->B, kMaxPairs);
-  if (d->flags & DPFT_COMBINE_ICP) return fail(DPFT_E_INVALID, "COMBINE_ICP not supported by this build yet");
+  if ((d->flags & DPFT_COMBINE_ICP) && !(d->icp_weight == d->icp_weight))
+    return fail(DPFT_E_INVALID, "icp_weight is NaN");
   return DPFT_OK;
 }
 
-int check_tensors(const DpftLevelTensors* t) {
+int check_tensors(const DpftLevelTensors* t, uint32_t flags = 0) {
   if (!t || !t->f0 || !t->f1 || !t->s0 || !t->s1 || !t->invD0 || !t->invD1 || !t->K)
     return fail(DPFT_E_INVALID, "null tensor pointer");
+  if ((flags & DPFT_COMBINE_ICP) && (!t->depth0 || !t->depth1))
+    return fail(DPFT_E_INVALID, "COMBINE_ICP needs depth0 and depth1");
   return DPFT_OK;
 }
 
@@ -1298,11 +1434,18 @@ int check_tensors(const DpftLevelTensors* t) {
 size_t prec_bytes(const DpftLevelDesc& d) { return ((size_t)d.B * kPRec * sizeof(double) + 255) & ~(size_t)255; }
 
 // reduce-kernel record slots: B * nbpp <= max(kMaxGrid, B)
-size_t ws_need(const DpftLevelDesc& d) {
+size_t rec_bytes(const DpftLevelDesc& d) {
   const Geometry g = plan(d);
   const size_t slots = std::max<size_t>(std::max<size_t>(kMaxGrid, d.B), (size_t)g.nblocks);
-  return kCtrlBytes + prec_bytes(d) + slots * kRec * sizeof(float);
+  return (slots * kRec * sizeof(float) + 255) & ~(size_t)255;
 }
+
+// COMBINE_ICP: frame-1 normal map [B,3,H,W] after the records
+size_t nrm_bytes(const DpftLevelDesc& d) {
+  return (d.flags & DPFT_COMBINE_ICP) ? (size_t)d.B * 3 * d.H * d.W * sizeof(float) : 0;
+}
+
+size_t ws_need(const DpftLevelDesc& d) { return kCtrlBytes + prec_bytes(d) + rec_bytes(d) + nrm_bytes(d); }
 
 IterParams make_params(const DpftLevelDesc& d, const DpftLevelTensors& tt, const Geometry& g, const float* R,
                        const float* t, void* ws) {
@@ -1315,6 +1458,12 @@ IterParams make_params(const DpftLevelDesc& d, const DpftLevelTensors& tt, const
   p.invD1 = tt.invD1;
   p.mask0 = tt.mask0;
   p.mask1 = tt.mask1;
+  p.depth0 = tt.depth0;
+  p.depth1 = tt.depth1;
+  p.nrm1 = (d.flags & DPFT_COMBINE_ICP)
+               ? reinterpret_cast<const float*>(static_cast<char*>(ws) + kCtrlBytes + prec_bytes(d) + rec_bytes(d))
+               : nullptr;
+  p.icp_w = d.icp_weight;
   p.K = tt.K;
   p.R = R;
   p.t = t;
@@ -1355,13 +1504,29 @@ int hip_check(const char* what) {
   return DPFT_OK;
 }
 
-int launch_minmax(const DpftLevelDesc& d, const DpftLevelTensors& tt, void* ws, hipStream_t st) {
-  if ((d.flags & DPFT_REMOVE_TRU_SIGMA) == 0) return DPFT_OK;  // extrema unused
-  uint32_t* ctrl = reinterpret_cast<uint32_t*>(ws);
-  const size_t n = (size_t)d.B * d.Cs * d.H * d.W;
+int minmax_into(const float* src, size_t n, uint32_t* ctrl, int slot, hipStream_t st) {
   const int grid = (int)std::min<size_t>((n + kThreads * 16 - 1) / (kThreads * 16), kMaxMMBlocks);
-  hipLaunchKernelGGL(minmax_kernel, dim3(grid), dim3(kThreads), 0, st, tt.s0, n, ctrl);
+  hipLaunchKernelGGL(minmax_kernel, dim3(grid), dim3(kThreads), 0, st, src, n, ctrl, slot);
   return hip_check("minmax_kernel");
+}
+
+// Pose-independent per-level pre-passes (first iteration of a level):
+// sigma0 batch extrema (truncated sigma), depth1 batch extrema + normal map (ICP).
+int launch_minmax(const DpftLevelDesc& d, const DpftLevelTensors& tt, void* ws, hipStream_t st) {
+  uint32_t* ctrl = reinterpret_cast<uint32_t*>(ws);
+  int rc;
+  if (d.flags & DPFT_REMOVE_TRU_SIGMA) {
+    if ((rc = minmax_into(tt.s0, (size_t)d.B * d.Cs * d.H * d.W, ctrl, kCtlMin, st))) return rc;
+  }
+  if (d.flags & DPFT_COMBINE_ICP) {
+    const size_t n = (size_t)d.B * d.H * d.W;
+    if ((rc = minmax_into(tt.depth1, n, ctrl, kCtlD1Min, st))) return rc;
+    float* nrm = reinterpret_cast<float*>(static_cast<char*>(ws) + kCtrlBytes + prec_bytes(d) + rec_bytes(d));
+    hipLaunchKernelGGL(icp_normals_kernel, dim3((unsigned)((n + kThreads - 1) / kThreads)), dim3(kThreads), 0, st,
+                       tt.depth1, tt.K, d.B, d.H, d.W, ctrl + kCtlD1Min, nrm);
+    if ((rc = hip_check("icp_normals_kernel"))) return rc;
+  }
+  return DPFT_OK;
 }
 
 // Workgroups of `kernel` the current device holds at once (cached per kernel and device).
@@ -1386,21 +1551,27 @@ int resident_blocks(const void* kernel) {
   return n;
 }
 
-template <int CT, bool CS1, bool TRU>
+template <int CT, bool CS1, bool TRU, bool ICP>
 int launch_reduce_k(IterParams p, hipStream_t st) {
-  const void* k = reinterpret_cast<const void*>(&ic_reduce_kernel<CT, CS1, TRU>);
+  const void* k = reinterpret_cast<const void*>(&ic_reduce_kernel<CT, CS1, TRU, ICP>);
   const int cap = resident_blocks(k);
   if (cap <= 0) return fail(DPFT_E_HIP, "occupancy query failed");
   p.nbpp = std::max(1, std::min(cap / p.B, p.per_pair));
   p.fin.nbpp = p.nbpp;
-  hipLaunchKernelGGL((ic_reduce_kernel<CT, CS1, TRU>), dim3(p.B * p.nbpp), dim3(kThreads), 0, st, p);
+  hipLaunchKernelGGL((ic_reduce_kernel<CT, CS1, TRU, ICP>), dim3(p.B * p.nbpp), dim3(kThreads), 0, st, p);
   return DPFT_OK;
 }
 
 template <int CT, bool CS1>
 int launch_reduce_t(const IterParams& p, hipStream_t st) {
-  return (p.flags & DPFT_REMOVE_TRU_SIGMA) ? launch_reduce_k<CT, CS1, true>(p, st)
-                                           : launch_reduce_k<CT, CS1, false>(p, st);
+  const bool tru = (p.flags & DPFT_REMOVE_TRU_SIGMA) != 0;
+  if (p.flags & DPFT_COMBINE_ICP) {
+    if constexpr (CS1 || CT == 0)
+      return tru ? launch_reduce_k<CT, CS1, true, true>(p, st) : launch_reduce_k<CT, CS1, false, true>(p, st);
+    else
+      return fail(DPFT_E_INVALID, "internal: no ICP instantiation for C=%d, Cs=C", CT);
+  }
+  return tru ? launch_reduce_k<CT, CS1, true, false>(p, st) : launch_reduce_k<CT, CS1, false, false>(p, st);
 }
 
 int launch_reduce(const IterParams& p, hipStream_t st) {
@@ -1413,10 +1584,14 @@ int launch_reduce(const IterParams& p, hipStream_t st) {
       default: rc = launch_reduce_t<0, true>(p, st); break;
     }
   } else {
-    switch (p.C) {
-      case 8: rc = launch_reduce_t<8, false>(p, st); break;
-      case 32: rc = launch_reduce_t<32, false>(p, st); break;
-      default: rc = launch_reduce_t<0, false>(p, st); break;
+    if (p.flags & DPFT_COMBINE_ICP) {
+      rc = launch_reduce_t<0, false>(p, st);
+    } else {
+      switch (p.C) {
+        case 8: rc = launch_reduce_t<8, false>(p, st); break;
+        case 32: rc = launch_reduce_t<32, false>(p, st); break;
+        default: rc = launch_reduce_t<0, false>(p, st); break;
+      }
     }
   }
   if (rc) return rc;
@@ -1427,7 +1602,7 @@ int iterate_impl(const DpftLevelDesc* desc, const DpftLevelTensors* tt, float* R
                  float* jtr_out, int32_t* invalid_out, int first, void* ws, size_t ws_bytes, hipStream_t st) {
   int rc = check_desc(desc);
   if (rc) return rc;
-  if ((rc = check_tensors(tt))) return rc;
+  if ((rc = check_tensors(tt, desc->flags))) return rc;
   if (!R || !t || !ws) return fail(DPFT_E_INVALID, "null pose / workspace");
   if (ws_bytes < ws_need(*desc)) return fail(DPFT_E_WORKSPACE, "workspace %zu < %zu", ws_bytes, ws_need(*desc));
   const Geometry g = plan(*desc);
@@ -1475,7 +1650,7 @@ int dpft_ic_residual_level(const DpftLevelDesc* desc, const DpftLevelTensors* tt
                            float* loss, void* ws, size_t ws_bytes, void* hip_stream) {
   int rc = check_desc(desc);
   if (rc) return rc;
-  if ((rc = check_tensors(tt))) return rc;
+  if ((rc = check_tensors(tt, desc->flags))) return rc;
   if (!R || !t || !loss || !ws) return fail(DPFT_E_INVALID, "null pose / loss / workspace");
   if (ws_bytes < ws_need(*desc)) return fail(DPFT_E_WORKSPACE, "workspace %zu < %zu", ws_bytes, ws_need(*desc));
   hipStream_t st = static_cast<hipStream_t>(hip_stream);
@@ -1483,10 +1658,18 @@ int dpft_ic_residual_level(const DpftLevelDesc* desc, const DpftLevelTensors* tt
   if ((rc = launch_minmax(*desc, *tt, ws, st))) return rc;
   IterParams p = make_params(*desc, *tt, g, R, t, ws);
   p.fin.loss_out = loss;
-  if (p.Cs == 1)
-    hipLaunchKernelGGL(ic_residual_kernel<true>, dim3(p.nblocks), dim3(kThreads), 0, st, p);
-  else
-    hipLaunchKernelGGL(ic_residual_kernel<false>, dim3(p.nblocks), dim3(kThreads), 0, st, p);
+  const bool icp = (desc->flags & DPFT_COMBINE_ICP) != 0;
+  if (p.Cs == 1) {
+    if (icp)
+      hipLaunchKernelGGL((ic_residual_kernel<true, true>), dim3(p.nblocks), dim3(kThreads), 0, st, p);
+    else
+      hipLaunchKernelGGL((ic_residual_kernel<true, false>), dim3(p.nblocks), dim3(kThreads), 0, st, p);
+  } else {
+    if (icp)
+      hipLaunchKernelGGL((ic_residual_kernel<false, true>), dim3(p.nblocks), dim3(kThreads), 0, st, p);
+    else
+      hipLaunchKernelGGL((ic_residual_kernel<false, false>), dim3(p.nblocks), dim3(kThreads), 0, st, p);
+  }
   return hip_check("ic_residual_kernel");
 }
 
@@ -1494,7 +1677,7 @@ int dpft_ic_reduce_only(const DpftLevelDesc* desc, const DpftLevelTensors* tt, c
                         void* ws, size_t ws_bytes, void* hip_stream) {
   int rc = check_desc(desc);
   if (rc) return rc;
-  if ((rc = check_tensors(tt))) return rc;
+  if ((rc = check_tensors(tt, desc->flags))) return rc;
   if (ws_bytes < ws_need(*desc)) return fail(DPFT_E_WORKSPACE, "workspace %zu < %zu", ws_bytes, ws_need(*desc));
   const Geometry g = plan(*desc);
   return launch_reduce(make_params(*desc, *tt, g, R, t, ws), static_cast<hipStream_t>(hip_stream));
@@ -1504,7 +1687,7 @@ int dpft_ic_debug_pixels(const DpftLevelDesc* desc, const DpftLevelTensors* tt, 
                          float* out, void* ws, size_t ws_bytes, void* hip_stream) {
   int rc = check_desc(desc);
   if (rc) return rc;
-  if ((rc = check_tensors(tt))) return rc;
+  if ((rc = check_tensors(tt, desc->flags))) return rc;
   if (!out || ws_bytes < ws_need(*desc)) return fail(DPFT_E_INVALID, "null output or small workspace");
   const Geometry g = plan(*desc);
   const IterParams p = make_params(*desc, *tt, g, R, t, ws);

@@ -50,7 +50,7 @@ def _run_hip_trace(name, dev):
 
 
 FEATURE_CASES = ["cfg1_160x120_c8", "cfg1b_160x120_c8_f04", "batch4_160x120_c8", "masks_160x120_c8",
-                 "cfg2_640x480_c32"]
+                 "cfg2_640x480_c32", "icp_160x120_c8"]
 
 
 @pytest.mark.parametrize("name", FEATURE_CASES)
@@ -75,7 +75,7 @@ def test_hip_matches_reference_golden(name):
     assert (trace[0]["invalid"] == z["f32_invalid"][0]).all(), (trace[0]["invalid"], z["f32_invalid"][0])
 
 
-@pytest.mark.parametrize("name", ["cfg1_160x120_c8", "batch4_160x120_c8", "masks_160x120_c8"])
+@pytest.mark.parametrize("name", ["cfg1_160x120_c8", "batch4_160x120_c8", "masks_160x120_c8", "icp_160x120_c8"])
 def test_hip_residual_loss(name):
     from deep_prob_feature_track_amd import ic
     dev = _dev()
@@ -87,7 +87,8 @@ def test_hip_residual_loss(name):
     K = torch.from_numpy(case["K"]).to(dev) / 2 ** (L - 1)
     loss = ic.residual_level((R, t), d["f0"], d["f1"], d["invD0"], d["invD1"], K, d["s0"], d["s1"],
                              remove_tru_sigma=bool(z["opt_remove_tru_sigma"]), obj_mask0=d.get("mask0"),
-                             obj_mask1=d.get("mask1"))
+                             obj_mask1=d.get("mask1"), depth0=d.get("depth0"), depth1=d.get("depth1"),
+                             combine_icp=bool(z["opt_combine_icp"]))
     np.testing.assert_allclose(loss.cpu().numpy(), z["f32_loss_start"][0], rtol=2e-5)
 
 
@@ -215,3 +216,42 @@ def test_nonfinite_raises_assertion():
     pose = (torch.eye(3, device=dev)[None], torch.zeros(1, 3, 1, device=dev))
     with pytest.raises(AssertionError):
         ic.solve_level(pose, f0, f1, invD0, invD1, K, z, z, iters=1)
+
+
+@pytest.mark.parametrize("B,C,Cs,H,W,tru,masks", [
+    (2, 8, 1, 60, 80, True, False),
+    (1, 16, 1, 48, 64, False, True),
+    (2, 5, 5, 37, 70, True, True),      # generic C, per-channel sigma
+])
+def test_hip_icp_matches_oracle_random(B, C, Cs, H, W, tru, masks):
+    """combine_ICP (algorithms.py:668-689, 916-997) vs the fp32 oracle on smooth random scenes."""
+    import torch.nn.functional as F
+    from deep_prob_feature_track_amd import ic
+    from oracle import ic_oracle as O
+    dev = _dev()
+    f0, f1, s0, s1, _, _, K, m0, m1 = _random_case(B, C, Cs, H, W, seed=B * 7 + C * 3 + W, masks=masks)
+    g = torch.Generator().manual_seed(W + H)
+    smooth = lambda: F.interpolate(torch.rand(B, 1, 6, 8, generator=g), size=(H, W), mode="bilinear",  # noqa: E731
+                                   align_corners=True)
+    depth0 = 1.0 + 2.0 * smooth()
+    depth1 = depth0 + 0.01 * smooth()
+    invD0, invD1 = 1.0 / depth0, 1.0 / depth1
+    R = torch.eye(3).repeat(B, 1, 1)
+    t = torch.zeros(B, 3, 1)
+    tr_o = []
+    O.solve_level(R, t, f0, f1, s0, s1, invD0, invD1, K, iters=3, remove_tru_sigma=tru, mask0=m0, mask1=m1,
+                  depth0=depth0, depth1=depth1, icp_scale=0.01, trace=tr_o)
+    cu = lambda a: a.to(dev) if a is not None else None  # noqa: E731
+    Rg, tg = R.to(dev), t.to(dev)
+    for it in range(3):
+        Rg, tg, jtj, jtr, inv = ic.iterate((Rg, tg), cu(f0), cu(f1), cu(invD0), cu(invD1), cu(K), cu(s0), cu(s1),
+                                           first=(it == 0), remove_tru_sigma=tru, obj_mask0=cu(m0),
+                                           obj_mask1=cu(m1), depth0=cu(depth0), depth1=cu(depth1),
+                                           combine_icp=True, icp_weight=0.01)
+        ref = tr_o[it]
+        if it == 0:
+            rel = (jtj.cpu() - ref["JtJ"]).abs().max() / ref["JtJ"].abs().max()
+            assert rel < 1e-4, f"JtJ rel {rel:.2e}"
+        dR = (Rg.cpu() - ref["R"]).abs().max().item()
+        dt = (tg.view(B, 3).cpu() - ref["t"]).abs().max().item()
+        assert dR <= SE3_TOL and dt <= SE3_TOL, f"iter {it}: |dR|={dR:.2e} |dt|={dt:.2e}"
