@@ -65,6 +65,9 @@ namespace {
 constexpr int kThreads = 256;          // 4 waves of 64
 constexpr int kTileW = 64;             // one wave = 64 consecutive pixels of a row
 constexpr int kRowsPerStep = 4;        // one row per wave per step
+#ifndef DPFT_RING
+#define DPFT_RING 2
+#endif
 #ifndef DPFT_CK
 #define DPFT_CK 2
 #endif
@@ -74,7 +77,8 @@ constexpr int kRowsPerStep = 4;        // one row per wave per step
 #ifndef DPFT_MIN_WAVES
 #define DPFT_MIN_WAVES 1
 #endif
-constexpr int kCK = DPFT_CK;           // channels staged in LDS per unit
+constexpr int kCK = DPFT_CK;           // channels per pipeline unit
+constexpr int kRing = DPFT_RING;       // load slots in flight ring (kRing - 1 units ahead)
 constexpr int kLdsW = kTileW + 2;      // 1-pixel halo each side
 constexpr int kLdsH = kRowsPerStep + 2;
 constexpr int kMaxSteps = DPFT_MAX_STEPS;  // up to 4 * kMaxSteps rows per workgroup
@@ -433,21 +437,39 @@ __device__ __forceinline__ float bld(Rsrc r, int voff, int soff) { return llvm_b
 __device__ __forceinline__ f32x2 bld2(Rsrc r, int voff, int soff) { return llvm_buf_load_f32x2(r, voff, soff, 0); }
 
 struct Gather4 {
-  float a, b, c, d;
+  float a, b, c, d;  // the two loaded pairs: (row y0: a, b), (row y1: c, d)
 };
 // The two taps of a sampling row are adjacent columns: one 8-byte load each.
-// The pair starts at min(x0, W-2) so it never leaves the row; at x0 = W-1 the
-// clamped neighbour x1 = x0 is the pair's second element, exactly like the
-// reference's border clamp.
+// The pair starts at min(x0, W-2) so it never leaves the row.  At x0 = W-1 the
+// clamped neighbour x1 = x0 is the pair's SECOND element and its weights ne, se
+// are exactly 0 (border clamp: ix = W-1 = x0); PairWeights moves nw, sw onto the
+// second element instead of selecting values per channel:
+// fma(p1y, sw, fma(p1x, 0, fma(p0y, nw, p0x * 0))) equals the reference's
+// fma(d, 0, fma(c, sw, fma(b, 0, a * nw))) bit for bit (finite inputs).
 __device__ __forceinline__ Gather4 gather4(Rsrc r, const Taps& t, int soff) {
   const f32x2 p0 = bld2(r, t.ob0 * 4, soff);
   const f32x2 p1 = bld2(r, t.ob1 * 4, soff);
   Gather4 g;
-  g.a = t.lo ? p0.x : p0.y;
+  g.a = p0.x;
   g.b = p0.y;
-  g.c = t.lo ? p1.x : p1.y;
+  g.c = p1.x;
   g.d = p1.y;
   return g;
+}
+struct PairWeights {
+  float w0, w1, w2, w3;
+};
+__device__ __forceinline__ PairWeights pair_weights(const Taps& t) {
+  PairWeights w;
+  w.w0 = t.lo ? t.nw : 0.0f;
+  w.w1 = t.lo ? t.ne : t.nw;
+  w.w2 = t.lo ? t.sw : 0.0f;
+  w.w3 = t.lo ? t.se : t.sw;
+  return w;
+}
+__device__ __forceinline__ float bilp(const Gather4& g, const PairWeights& w) {
+#pragma clang fp contract(off)
+  return __builtin_fmaf(g.d, w.w3, __builtin_fmaf(g.c, w.w2, __builtin_fmaf(g.b, w.w1, g.a * w.w0)));
 }
 
 // ---------------------------------------------------------------- stencil by DPP
@@ -461,10 +483,10 @@ __device__ __forceinline__ Gather4 gather4(Rsrc r, const Taps& t, int soff) {
 constexpr int kTileOut = kTileW - 2;  // output pixels per tile row
 
 __device__ __forceinline__ float lane_from_left(float v) {  // lane l gets lane l - 1
-  return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x138, 0xf, 0xf, false));
+  return __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), 0x138, 0xf, 0xf, true));
 }
 __device__ __forceinline__ float lane_from_right(float v) {  // lane l gets lane l + 1
-  return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x130, 0xf, 0xf, false));
+  return __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), 0x130, 0xf, 0xf, true));
 }
 
 // Unit-normalised Sobel from the three rows of this lane's column (algorithms.py:1852-1863).
@@ -907,7 +929,7 @@ __global__ __launch_bounds__(kThreads, DPFT_MIN_WAVES) void ic_reduce_kernel(Ite
   const float g0min = TRU ? dec_ord(p.ext[0]) : 0.f, g0max = TRU ? dec_ord(p.ext[1]) : 0.f;
   const uint32_t planeB = (uint32_t)HW * 4u;
   const int nch = (C + kCK - 1) / kCK;
-  const int npair = (nch + 1) >> 1;                 // chunk pairs per step (odd counts get an empty chunk)
+  const int nunits = (nch + kRing - 1) / kRing * kRing;  // units per step, padded to the ring (empty tail units)
 
   const float fx = p.K[4 * b + 0], fy = p.K[4 * b + 1], cx = p.K[4 * b + 2], cy = p.K[4 * b + 3];
   float Rm[9], tv[3];
@@ -972,6 +994,7 @@ __global__ __launch_bounds__(kThreads, DPFT_MIN_WAVES) void ic_reduce_kernel(Ite
     // ---- frame: warp, taps, occlusion, masks (geometry.py:291-350, algorithms.py:1999-2008)
     const Warp wp = warp_point(xc, y, d, Rm, tv, fx, fy, cx, cy);
     const Taps tp = make_taps(wp.u, wp.v, H, W);
+    const PairWeights pw = pair_weights(tp);
     const Gather4 gd1 = gather4(rd1, tp, 0);
     const bool m0 = m0b ? (m0b[y * W + xc] != 0) : true;
     const float m1 = m1b ? bil_u8(m1b, tp) : 1.0f;
@@ -984,25 +1007,39 @@ __global__ __launch_bounds__(kThreads, DPFT_MIN_WAVES) void ic_reduce_kernel(Ite
       gs1 = gather4(rs1, tp, 0);
     }
 
-    ChanLoads LE[kCK], LO[kCK];
+    ChanLoads S[kRing][kCK];
     auto issue = [&](ChanLoads (&L)[kCK], int k) {
 #pragma unroll
       for (int cc = 0; cc < kCK; ++cc) {
         const int c = k * kCK + cc;
         if (c < C) {
           const int po = c * (int)planeB;
+#if DPFT_ABL_ROWS
+          L[cc].m = bld(rf0, colv, po + rM);
+          L[cc].t = L[cc].m;
+          L[cc].b = L[cc].m;
+#else
           L[cc].t = bld(rf0, colv, po + rT);
           L[cc].m = bld(rf0, colv, po + rM);
           L[cc].b = bld(rf0, colv, po + rB);
+#endif
+#if DPFT_ABL_GATHER
+          L[cc].g.a = bld(rf1, colv, po + rM);
+          L[cc].g.b = L[cc].g.a;
+          L[cc].g.c = L[cc].g.a;
+          L[cc].g.d = L[cc].g.a;
+#else
           L[cc].g = gather4(rf1, tp, po);
+#endif
         }
       }
     };
-    issue(LE, 0);
+#pragma unroll
+    for (int r = 0; r + 1 < kRing; ++r) issue(S[r], r);
 
     bool invalid;
     {
-      const float d1w = bil4(gd1.a, gd1.b, gd1.c, gd1.d, tp);
+      const float d1w = bilp(gd1, pw);
       const bool ok = (wp.iz > d1w - 0.1f) && (wp.u > 0.0f) && (wp.u < (float)W) && (wp.v > 0.0f) &&
                       (wp.v < (float)H);
       invalid = !ok || !out_lane || !m0 || !(m1 > 0.0f);
@@ -1010,17 +1047,17 @@ __global__ __launch_bounds__(kThreads, DPFT_MIN_WAVES) void ic_reduce_kernel(Ite
     float sr0 = 0.f, srmin = 0.f, srmax = 0.f, inv_s = 0.f, kk = 0.f, hx = 0.f, hy = 0.f;
     if (CS1) {
       sobel_cols(s0t, s0m, s0b_, hx, hy);
-      sr0 = bil4(gs1.a, gs1.b, gs1.c, gs1.d, tp);
+      sr0 = bilp(gs1, pw);
       srmin = srmax = sr0;
       const float sg = sqrtf(sr0 * sr0 + s0m * s0m);
-      inv_s = 1.0f / sg;
+      inv_s = __builtin_amdgcn_rcpf(sg);  // 1 ulp; r * (1/sigma) is a continuous weight
       kk = s0m * (inv_s * inv_s * inv_s);
       if (TRU) invalid = invalid || (s0m == g0min) || (s0m == g0max);
     }
     float Saa = 0.f, Sab = 0.f, Sbb = 0.f, Sa = 0.f, Sb = 0.f, Sar = 0.f, Sbr = 0.f;
 
     auto unit = [&](int k, ChanLoads (&cur)[kCK], ChanLoads (&nxt)[kCK]) {
-      if (k + 1 < 2 * npair) issue(nxt, k + 1);
+      if (k + kRing - 1 < nunits) issue(nxt, k + kRing - 1);
 #pragma unroll
       for (int cc = 0; cc < kCK; ++cc) {
         const int c = k * kCK + cc;
@@ -1046,7 +1083,7 @@ __global__ __launch_bounds__(kThreads, DPFT_MIN_WAVES) void ic_reduce_kernel(Ite
             srmax = fmaxf(srmax, src);
           }
         }
-        const float frv = bil4(cur[cc].g.a, cur[cc].g.b, cur[cc].g.c, cur[cc].g.d, tp);
+        const float frv = bilp(cur[cc].g, pw);
         const float r = frv - f0v;
         const float rw = r * is_c;
         const float rk = r * kk_c;
@@ -1064,9 +1101,9 @@ __global__ __launch_bounds__(kThreads, DPFT_MIN_WAVES) void ic_reduce_kernel(Ite
     };
 
 #pragma unroll 1
-    for (int kp = 0; kp < npair; ++kp) {
-      unit(2 * kp, LE, LO);
-      unit(2 * kp + 1, LO, LE);
+    for (int kb = 0; kb < nunits; kb += kRing) {
+#pragma unroll
+      for (int r = 0; r < kRing; ++r) unit(kb + r, S[r], S[(r + kRing - 1) % kRing]);
     }
     Sa = -Sa;
     Sb = -Sb;
