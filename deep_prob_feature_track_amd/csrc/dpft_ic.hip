@@ -739,86 +739,155 @@ __device__ void block_minmax2(float& mn_a, float& mx_a, float& mn_b, float& mx_b
 }
 
 // Run by the last workgroup of pair b: reduce its per-workgroup records into one
-// fp64 pair record.  Thread (j, i) sums component i over records j, j+8, ...
-// (4 loads in flight), the 8 partials are then added in a fixed order.  The
-// truncated-sigma corrections of the workgroups that attain the pair's extremum
-// of sigma_r (channel 0) are kept apart: whether they apply depends on the
-// batch-global extremum, known only when every pair is done.
+// fp64 pair record in ONE load round trip.  Threads 0-127 take the 21 JtJ
+// components of record tid (+128, ...), threads 128-255 the 6 JtR components, the
+// invalid count and the truncated-sigma extremum fields; per-thread fp64 sums and
+// online extremum merges (fixed record order), then fixed xor-tree wave
+// reductions and a fixed two-wave combine: deterministic for any finishing order.
+// The corrections of the records attaining the pair's extremum of sigma_r ch0 are
+// kept apart: whether they apply depends on the batch-global extremum.
+struct ExtD {
+  float v;     // extremum of sigma_r channel 0
+  double c[7]; // JtR corrections (6) + count of the pixels attaining it
+};
+template <bool MIN>
+__device__ __forceinline__ void extd_merge(ExtD& a, float v, const double* c) {
+  if (MIN ? (v < a.v) : (v > a.v)) {
+    a.v = v;
+#pragma unroll
+    for (int i = 0; i < 7; ++i) a.c[i] = c[i];
+  } else if (v == a.v) {
+#pragma unroll
+    for (int i = 0; i < 7; ++i) a.c[i] += c[i];
+  }
+}
+template <bool MIN>
+__device__ __forceinline__ void extd_wave_reduce(ExtD& e) {
+  for (int off = 32; off > 0; off >>= 1) {
+    const float v = __shfl_xor(e.v, off);
+    double c[7];
+#pragma unroll
+    for (int i = 0; i < 7; ++i) c[i] = __shfl_xor(e.c[i], off);
+    // both partners apply the same (commutative) rule to the same pair of values
+    extd_merge<MIN>(e, v, c);
+  }
+}
+
 __device__ void pair_reduce(const FinParams& q, int b) {
-  __shared__ double part[8][32], pmn[8][8], pmx[8][8];
-  const int tid = threadIdx.x, i = tid & 31, j = tid >> 5;
+  __shared__ double shs[2][21];
+  __shared__ double shr[2][7];
+  __shared__ float shv[2][4];
+  __shared__ double shc[2][2][7];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const bool tru = (q.flags & DPFT_REMOVE_TRU_SIGMA) != 0;
   const float* rec = q.rec + (size_t)b * q.nbpp * kRec;  // slots of pair b's workgroups
   const int n = q.nbpp;
-  float mn_all = INFINITY, mx_all = -INFINITY, mn0 = INFINITY, mx0 = -INFINITY;
-  if (tru) {
-    float a = INFINITY, c = -INFINITY;
-    for (int k = tid; k < n; k += kThreads) {
+  double* pr = q.prec + (size_t)b * kPRec;
+  if (tid < 128) {
+    double s[21];
+#pragma unroll
+    for (int i = 0; i < 21; ++i) s[i] = 0.0;
+    for (int k = tid; k < n; k += 128) {
+      float v[21];
       const float* r = rec + (size_t)k * kRec;
-      mn_all = fminf(mn_all, ld_ag(r + R_MN_ALL));
-      mx_all = fmaxf(mx_all, ld_ag(r + R_MX_ALL));
-      a = fminf(a, ld_ag(r + R_MN0));
-      c = fmaxf(c, ld_ag(r + R_MX0));
-    }
-    mn0 = a;
-    mx0 = c;
-    block_minmax2(mn_all, mx_all, mn0, mx0);
-  }
-  const int ci = i - 21;  // correction slot (0..6) of components 21..27
-  double acc = 0.0, cmn = 0.0, cmx = 0.0;
-  if (i < 28) {
-    for (int k0 = j; k0 < n; k0 += 32) {
-      float v[4], m[4], x[4], cn[4], cx[4];
 #pragma unroll
-      for (int u = 0; u < 4; ++u) {
-        const int k = k0 + 8 * u;
-        const float* r = rec + (size_t)min(k, n - 1) * kRec;
-        const bool ok = k < n;
-        v[u] = ok ? ld_ag(r + i) : 0.0f;
-        if (tru && i >= 21) {
-          m[u] = ok ? ld_ag(r + R_MN0) : NAN;
-          x[u] = ok ? ld_ag(r + R_MX0) : NAN;
-          cn[u] = ld_ag(r + R_CMN + ci);  // R_CMN + 6 == R_NMN
-          cx[u] = ld_ag(r + R_CMX + ci);  // R_CMX + 6 == R_NMX
+      for (int i = 0; i < 21; ++i) v[i] = ld_ag(r + i);
+#pragma unroll
+      for (int i = 0; i < 21; ++i) s[i] += (double)v[i];
+    }
+#pragma unroll
+    for (int i = 0; i < 21; ++i) s[i] = wave_sum_d(s[i]);
+    if (lane == 0)
+#pragma unroll
+      for (int i = 0; i < 21; ++i) shs[wave][i] = s[i];
+  } else {
+    double s[7];
+#pragma unroll
+    for (int i = 0; i < 7; ++i) s[i] = 0.0;
+    ExtD emn, emx;
+    emn.v = INFINITY;
+    emx.v = -INFINITY;
+#pragma unroll
+    for (int i = 0; i < 7; ++i) emn.c[i] = emx.c[i] = 0.0;
+    float mn_all = INFINITY, mx_all = -INFINITY;
+    for (int k = tid - 128; k < n; k += 128) {
+      const float* r = rec + (size_t)k * kRec;
+      float v[7], cn[7], cx[7], m0 = 0.f, x0 = 0.f, ma = 0.f, xa = 0.f;
+#pragma unroll
+      for (int i = 0; i < 7; ++i) v[i] = ld_ag(r + 21 + i);
+      if (tru) {
+#pragma unroll
+        for (int i = 0; i < 7; ++i) {
+          cn[i] = ld_ag(r + R_CMN + i);  // R_CMN + 6 == R_NMN
+          cx[i] = ld_ag(r + R_CMX + i);  // R_CMX + 6 == R_NMX
         }
+        m0 = ld_ag(r + R_MN0);
+        x0 = ld_ag(r + R_MX0);
+        ma = ld_ag(r + R_MN_ALL);
+        xa = ld_ag(r + R_MX_ALL);
       }
 #pragma unroll
-      for (int u = 0; u < 4; ++u) {
-        acc += (double)v[u];
-        if (tru && i >= 21) {
-          if (m[u] == mn0) cmn += (double)cn[u];
-          if (x[u] == mx0) cmx += (double)cx[u];
+      for (int i = 0; i < 7; ++i) s[i] += (double)v[i];
+      if (tru) {
+        double dn[7], dx[7];
+#pragma unroll
+        for (int i = 0; i < 7; ++i) {
+          dn[i] = (double)cn[i];
+          dx[i] = (double)cx[i];
         }
+        extd_merge<true>(emn, m0, dn);
+        extd_merge<false>(emx, x0, dx);
+        mn_all = fminf(mn_all, ma);
+        mx_all = fmaxf(mx_all, xa);
       }
     }
-  }
-  part[j][i] = acc;
-  if (i >= 21 && i < 28) {
-    pmn[j][ci] = cmn;
-    pmx[j][ci] = cmx;
+#pragma unroll
+    for (int i = 0; i < 7; ++i) s[i] = wave_sum_d(s[i]);
+    if (tru) {
+      extd_wave_reduce<true>(emn);
+      extd_wave_reduce<false>(emx);
+      for (int off = 32; off > 0; off >>= 1) {
+        mn_all = fminf(mn_all, __shfl_xor(mn_all, off));
+        mx_all = fmaxf(mx_all, __shfl_xor(mx_all, off));
+      }
+    }
+    const int w = wave - 2;
+    if (lane == 0) {
+#pragma unroll
+      for (int i = 0; i < 7; ++i) {
+        shr[w][i] = s[i];
+        shc[w][0][i] = emn.c[i];
+        shc[w][1][i] = emx.c[i];
+      }
+      shv[w][0] = emn.v;
+      shv[w][1] = emx.v;
+      shv[w][2] = mn_all;
+      shv[w][3] = mx_all;
+    }
   }
   __syncthreads();
-  double* pr = q.prec + (size_t)b * kPRec;
-  if (tid < 28) {
-    double v = part[0][tid];
+  if (tid < 21) {
+    st_ag(pr + P_S + tid, shs[0][tid] + shs[1][tid]);
+  } else if (tid < 28) {
+    st_ag(pr + P_S + tid, shr[0][tid - 21] + shr[1][tid - 21]);
+  } else if (tid == 64) {
+    ExtD e;
+    e.v = shv[0][0];
 #pragma unroll
-    for (int m = 1; m < 8; ++m) v += part[m][tid];
-    st_ag(pr + P_S + tid, (double)(v));
-  } else if (tid >= 32 && tid < 39) {
-    double v = pmn[0][tid - 32];
+    for (int i = 0; i < 7; ++i) e.c[i] = shc[0][0][i];
+    extd_merge<true>(e, shv[1][0], shc[1][0]);
+    for (int i = 0; i < 7; ++i) st_ag(pr + P_CMN + i, e.c[i]);
+    st_ag(pr + P_MN0, (double)e.v);
+    st_ag(pr + P_MN_ALL, (double)fminf(shv[0][2], shv[1][2]));
+  } else if (tid == 128) {
+    ExtD e;
+    e.v = shv[0][1];
 #pragma unroll
-    for (int m = 1; m < 8; ++m) v += pmn[m][tid - 32];
-    st_ag(pr + P_CMN + tid - 32, (double)(v));
-  } else if (tid >= 64 && tid < 71) {
-    double v = pmx[0][tid - 64];
-#pragma unroll
-    for (int m = 1; m < 8; ++m) v += pmx[m][tid - 64];
-    st_ag(pr + P_CMX + tid - 64, (double)(v));
-  } else if (tid == 96) {
-    st_ag(pr + P_MN_ALL, (double)(mn_all));
-    st_ag(pr + P_MN0, (double)(mn0));
-    st_ag(pr + P_MX_ALL, (double)(mx_all));
-    st_ag(pr + P_MX0, (double)(mx0));
+    for (int i = 0; i < 7; ++i) e.c[i] = shc[0][1][i];
+    extd_merge<false>(e, shv[1][1], shc[1][1]);
+    for (int i = 0; i < 7; ++i) st_ag(pr + P_CMX + i, e.c[i]);
+    st_ag(pr + P_MX0, (double)e.v);
+    st_ag(pr + P_MX_ALL, (double)fmaxf(shv[0][3], shv[1][3]));
   }
 }
 
@@ -1014,23 +1083,10 @@ __global__ __launch_bounds__(kThreads, DPFT_MIN_WAVES) void ic_reduce_kernel(Ite
         const int c = k * kCK + cc;
         if (c < C) {
           const int po = c * (int)planeB;
-#if DPFT_ABL_ROWS
-          L[cc].m = bld(rf0, colv, po + rM);
-          L[cc].t = L[cc].m;
-          L[cc].b = L[cc].m;
-#else
           L[cc].t = bld(rf0, colv, po + rT);
           L[cc].m = bld(rf0, colv, po + rM);
           L[cc].b = bld(rf0, colv, po + rB);
-#endif
-#if DPFT_ABL_GATHER
-          L[cc].g.a = bld(rf1, colv, po + rM);
-          L[cc].g.b = L[cc].g.a;
-          L[cc].g.c = L[cc].g.a;
-          L[cc].g.d = L[cc].g.a;
-#else
           L[cc].g = gather4(rf1, tp, po);
-#endif
         }
       }
     };
