@@ -37,6 +37,7 @@ class LevelTensors(ctypes.Structure):
 
 
 EXPORTS = ("dpft_workspace_size", "dpft_ic_solve_level", "dpft_ic_iterate", "dpft_ic_residual_level",
+           "dpft_residual_poses_workspace_size", "dpft_ic_residual_poses",
            "dpft_ic_reduce_only", "dpft_ic_debug_pixels", "dpft_version", "dpft_last_error")
 
 _lib = None
@@ -60,6 +61,10 @@ def lib():
     L.dpft_ic_iterate.restype = ctypes.c_int
     L.dpft_ic_residual_level.argtypes = [P(LevelDesc), P(LevelTensors), vp, vp, vp, vp, sz, vp]
     L.dpft_ic_residual_level.restype = ctypes.c_int
+    L.dpft_residual_poses_workspace_size.argtypes = [P(LevelDesc), ctypes.c_int32]
+    L.dpft_residual_poses_workspace_size.restype = sz
+    L.dpft_ic_residual_poses.argtypes = [P(LevelDesc), P(LevelTensors), ctypes.c_int32, vp, vp, vp, vp, sz, vp]
+    L.dpft_ic_residual_poses.restype = ctypes.c_int
     L.dpft_ic_reduce_only.argtypes = [P(LevelDesc), P(LevelTensors), vp, vp, vp, sz, vp]
     L.dpft_ic_reduce_only.restype = ctypes.c_int
     L.dpft_ic_debug_pixels.argtypes = [P(LevelDesc), P(LevelTensors), vp, vp, vp, vp, sz, vp]

@@ -1309,11 +1309,15 @@ __global__ __launch_bounds__(kThreads, DPFT_MIN_WAVES) void ic_reduce_kernel(Ite
 }
 
 // ============================================================ residual-only kernel
+// blockIdx.y = pose index: P poses per pair share the level's inputs; pose p
+// evaluates the batch of B pairs at R[p], t[p] (its own batch-global
+// truncated-sigma extrema, as one reference call per pose would).
 template <bool CS1, bool ICP>
 __global__ __launch_bounds__(kThreads) void ic_residual_kernel(IterParams p) {
   __shared__ float red[4][16];
   const int tid = threadIdx.x, lane = tid & 63, wave = wave_id();
   const int bid = xcd_remap(blockIdx.x, p.nblocks);
+  const int pi = blockIdx.y;
   const int tx = bid % p.tiles_x;
   const int rest = bid / p.tiles_x;
   const int ty = rest % p.tiles_y;
@@ -1322,8 +1326,8 @@ __global__ __launch_bounds__(kThreads) void ic_residual_kernel(IterParams p) {
   const bool tru = (p.flags & DPFT_REMOVE_TRU_SIGMA) != 0;
   const float fx = p.K[4 * b + 0], fy = p.K[4 * b + 1], cx = p.K[4 * b + 2], cy = p.K[4 * b + 3];
   float Rm[9], tv[3];
-  for (int k = 0; k < 9; ++k) Rm[k] = p.R[9 * b + k];
-  for (int k = 0; k < 3; ++k) tv[k] = p.t[3 * b + k];
+  for (int k = 0; k < 9; ++k) Rm[k] = p.R[9 * ((size_t)pi * p.B + b) + k];
+  for (int k = 0; k < 3; ++k) tv[k] = p.t[3 * ((size_t)pi * p.B + b) + k];
   const float g0min = dec_ord(p.ext[0]), g0max = dec_ord(p.ext[1]);
   const float* f0b = p.f0 + (size_t)b * C * HW;
   const float* f1b = p.f1 + (size_t)b * C * HW;
@@ -1392,7 +1396,7 @@ __global__ __launch_bounds__(kThreads) void ic_residual_kernel(IterParams p) {
   }
   __syncthreads();
   if (tid == 0) {
-    float* out = p.rec + (size_t)bid * kRec;
+    float* out = p.rec + ((size_t)pi * p.nblocks + bid) * kRec;
     float s = red[0][L_SUM], ni = red[0][L_NINV];
     float ma = red[0][L_MN_ALL], m0 = red[0][L_MN0], lm = red[0][L_LMN], nm = red[0][L_NMN];
     float xa = red[0][L_MX_ALL], x0v = red[0][L_MX0], lx = red[0][L_LMX], nx = red[0][L_NMX];
@@ -1410,7 +1414,12 @@ __global__ __launch_bounds__(kThreads) void ic_residual_kernel(IterParams p) {
     st_ag(out + L_MN_ALL, (float)(ma)); st_ag(out + L_MN0, (float)(m0)); st_ag(out + L_LMN, (float)(lm)); st_ag(out + L_NMN, (float)(nm));
     st_ag(out + L_MX_ALL, (float)(xa)); st_ag(out + L_MX0, (float)(x0v)); st_ag(out + L_LMX, (float)(lx)); st_ag(out + L_NMX, (float)(nx));
   }
-  if (block_is_last(p.ctrl + kCtlResDone, 1u, (uint32_t)p.nblocks)) finalize_loss(p.fin);
+  if (block_is_last(p.ctrl + kCtlPair + pi, 1u, (uint32_t)p.nblocks)) {
+    FinParams q = p.fin;
+    q.rec += (size_t)pi * p.nblocks * kRec;
+    q.loss_out += (size_t)pi * p.B;
+    finalize_loss(q);
+  }
 }
 
 
@@ -1533,12 +1542,24 @@ size_t rec_bytes(const DpftLevelDesc& d) {
   return (slots * kRec * sizeof(float) + 255) & ~(size_t)255;
 }
 
-// COMBINE_ICP: frame-1 normal map [B,3,H,W] after the records
+// COMBINE_ICP: frame-1 normal map [B,3,H,W] between the pair records and the
+// workgroup records (the latter grow with the number of poses of a residual call)
 size_t nrm_bytes(const DpftLevelDesc& d) {
   return (d.flags & DPFT_COMBINE_ICP) ? (size_t)d.B * 3 * d.H * d.W * sizeof(float) : 0;
 }
 
-size_t ws_need(const DpftLevelDesc& d) { return kCtrlBytes + prec_bytes(d) + rec_bytes(d) + nrm_bytes(d); }
+size_t ws_need(const DpftLevelDesc& d) {
+  return kCtrlBytes + prec_bytes(d) + ((nrm_bytes(d) + 255) & ~(size_t)255) + rec_bytes(d);
+}
+size_t nrm_offset(const DpftLevelDesc& d) { return kCtrlBytes + prec_bytes(d); }
+size_t rec_offset(const DpftLevelDesc& d) { return kCtrlBytes + prec_bytes(d) + ((nrm_bytes(d) + 255) & ~(size_t)255); }
+
+// residual evaluation of P poses: P x nblocks records (normal map after them)
+size_t ws_need_poses(const DpftLevelDesc& d, int P) {
+  const Geometry g = plan(d);
+  const size_t rec = ((size_t)P * g.nblocks * kRec * sizeof(float) + 255) & ~(size_t)255;
+  return rec_offset(d) + std::max(rec, rec_bytes(d));
+}
 
 IterParams make_params(const DpftLevelDesc& d, const DpftLevelTensors& tt, const Geometry& g, const float* R,
                        const float* t, void* ws) {
@@ -1553,9 +1574,8 @@ IterParams make_params(const DpftLevelDesc& d, const DpftLevelTensors& tt, const
   p.mask1 = tt.mask1;
   p.depth0 = tt.depth0;
   p.depth1 = tt.depth1;
-  p.nrm1 = (d.flags & DPFT_COMBINE_ICP)
-               ? reinterpret_cast<const float*>(static_cast<char*>(ws) + kCtrlBytes + prec_bytes(d) + rec_bytes(d))
-               : nullptr;
+  p.nrm1 = (d.flags & DPFT_COMBINE_ICP) ? reinterpret_cast<const float*>(static_cast<char*>(ws) + nrm_offset(d))
+                                        : nullptr;
   p.icp_w = d.icp_weight;
   p.K = tt.K;
   p.R = R;
@@ -1572,7 +1592,7 @@ IterParams make_params(const DpftLevelDesc& d, const DpftLevelTensors& tt, const
   p.flags = d.flags;
   p.ctrl = reinterpret_cast<uint32_t*>(ws);
   p.ext = p.ctrl + kCtlMin;
-  p.rec = reinterpret_cast<float*>(static_cast<char*>(ws) + kCtrlBytes + prec_bytes(d));
+  p.rec = reinterpret_cast<float*>(static_cast<char*>(ws) + rec_offset(d));
   p.row_groups = (d.H + kRowsPerStep - 1) / kRowsPerStep;
   p.per_pair = g.tiles_x * p.row_groups;
   p.nbpp = 0;  // set at launch from the kernel's resident capacity
@@ -1614,7 +1634,7 @@ int launch_minmax(const DpftLevelDesc& d, const DpftLevelTensors& tt, void* ws, 
   if (d.flags & DPFT_COMBINE_ICP) {
     const size_t n = (size_t)d.B * d.H * d.W;
     if ((rc = minmax_into(tt.depth1, n, ctrl, kCtlD1Min, st))) return rc;
-    float* nrm = reinterpret_cast<float*>(static_cast<char*>(ws) + kCtrlBytes + prec_bytes(d) + rec_bytes(d));
+    float* nrm = reinterpret_cast<float*>(static_cast<char*>(ws) + nrm_offset(d));
     hipLaunchKernelGGL(icp_normals_kernel, dim3((unsigned)((n + kThreads - 1) / kThreads)), dim3(kThreads), 0, st,
                        tt.depth1, tt.K, d.B, d.H, d.W, ctrl + kCtlD1Min, nrm);
     if ((rc = hip_check("icp_normals_kernel"))) return rc;
@@ -1710,6 +1730,35 @@ int iterate_impl(const DpftLevelDesc* desc, const DpftLevelTensors* tt, float* R
   return launch_reduce(p, st);
 }
 
+int residual_impl(const DpftLevelDesc* desc, const DpftLevelTensors* tt, int P, const float* R, const float* t,
+                  float* loss, void* ws, size_t ws_bytes, hipStream_t st) {
+  int rc = check_desc(desc);
+  if (rc) return rc;
+  if ((rc = check_tensors(tt, desc->flags))) return rc;
+  if (!R || !t || !loss || !ws) return fail(DPFT_E_INVALID, "null pose / loss / workspace");
+  if (P < 1 || P > kMaxPairs) return fail(DPFT_E_INVALID, "n_poses=%d outside [1, %d]", P, kMaxPairs);
+  if (ws_bytes < ws_need_poses(*desc, P))
+    return fail(DPFT_E_WORKSPACE, "workspace %zu < %zu", ws_bytes, ws_need_poses(*desc, P));
+  const Geometry g = plan(*desc);
+  if ((rc = launch_minmax(*desc, *tt, ws, st))) return rc;
+  IterParams p = make_params(*desc, *tt, g, R, t, ws);
+  p.fin.loss_out = loss;
+  const dim3 grid(p.nblocks, P);
+  const bool icp = (desc->flags & DPFT_COMBINE_ICP) != 0;
+  if (p.Cs == 1) {
+    if (icp)
+      hipLaunchKernelGGL((ic_residual_kernel<true, true>), grid, dim3(kThreads), 0, st, p);
+    else
+      hipLaunchKernelGGL((ic_residual_kernel<true, false>), grid, dim3(kThreads), 0, st, p);
+  } else {
+    if (icp)
+      hipLaunchKernelGGL((ic_residual_kernel<false, true>), grid, dim3(kThreads), 0, st, p);
+    else
+      hipLaunchKernelGGL((ic_residual_kernel<false, false>), grid, dim3(kThreads), 0, st, p);
+  }
+  return hip_check("ic_residual_kernel");
+}
+
 }  // namespace
 
 extern "C" {
@@ -1741,29 +1790,17 @@ int dpft_ic_solve_level(const DpftLevelDesc* desc, const DpftLevelTensors* tenso
 
 int dpft_ic_residual_level(const DpftLevelDesc* desc, const DpftLevelTensors* tt, const float* R, const float* t,
                            float* loss, void* ws, size_t ws_bytes, void* hip_stream) {
-  int rc = check_desc(desc);
-  if (rc) return rc;
-  if ((rc = check_tensors(tt, desc->flags))) return rc;
-  if (!R || !t || !loss || !ws) return fail(DPFT_E_INVALID, "null pose / loss / workspace");
-  if (ws_bytes < ws_need(*desc)) return fail(DPFT_E_WORKSPACE, "workspace %zu < %zu", ws_bytes, ws_need(*desc));
-  hipStream_t st = static_cast<hipStream_t>(hip_stream);
-  const Geometry g = plan(*desc);
-  if ((rc = launch_minmax(*desc, *tt, ws, st))) return rc;
-  IterParams p = make_params(*desc, *tt, g, R, t, ws);
-  p.fin.loss_out = loss;
-  const bool icp = (desc->flags & DPFT_COMBINE_ICP) != 0;
-  if (p.Cs == 1) {
-    if (icp)
-      hipLaunchKernelGGL((ic_residual_kernel<true, true>), dim3(p.nblocks), dim3(kThreads), 0, st, p);
-    else
-      hipLaunchKernelGGL((ic_residual_kernel<true, false>), dim3(p.nblocks), dim3(kThreads), 0, st, p);
-  } else {
-    if (icp)
-      hipLaunchKernelGGL((ic_residual_kernel<false, true>), dim3(p.nblocks), dim3(kThreads), 0, st, p);
-    else
-      hipLaunchKernelGGL((ic_residual_kernel<false, false>), dim3(p.nblocks), dim3(kThreads), 0, st, p);
-  }
-  return hip_check("ic_residual_kernel");
+  return residual_impl(desc, tt, 1, R, t, loss, ws, ws_bytes, static_cast<hipStream_t>(hip_stream));
+}
+
+size_t dpft_residual_poses_workspace_size(const DpftLevelDesc* desc, int32_t n_poses) {
+  if (check_desc(desc) || n_poses < 1 || n_poses > kMaxPairs) return 0;
+  return ws_need_poses(*desc, n_poses);
+}
+
+int dpft_ic_residual_poses(const DpftLevelDesc* desc, const DpftLevelTensors* tt, int32_t n_poses, const float* R,
+                           const float* t, float* loss, void* ws, size_t ws_bytes, void* hip_stream) {
+  return residual_impl(desc, tt, n_poses, R, t, loss, ws, ws_bytes, static_cast<hipStream_t>(hip_stream));
 }
 
 int dpft_ic_reduce_only(const DpftLevelDesc* desc, const DpftLevelTensors* tt, const float* R, const float* t,

@@ -151,6 +151,29 @@ def residual_level(pose, x0, x1, invD0, invD1, K, sigma0, sigma1, **kw):
     return loss
 
 
+def residual_poses(R, t, x0, x1, invD0, invD1, K, sigma0, sigma1, **kw):
+    """forward_residuals for P poses per pair in one launch: R [P,B,3,3], t [P,B,3(,1)] -> loss [P,B].
+
+    Each pose index is evaluated as one reference call over the batch (its own
+    batch-global truncated-sigma extrema)."""
+    c = LevelCall(x0, x1, invD0, invD1, K, sigma0, sigma1, iters=1, **kw)
+    P = R.shape[0]
+    if R.shape[1] != c.B or t.shape[:2] != (P, c.B):
+        raise ValueError(f"poses R {tuple(R.shape)}, t {tuple(t.shape)} do not match B={c.B}")
+    Rb = R.to(torch.float32).reshape(P, c.B, 9).contiguous()
+    tb = t.to(torch.float32).reshape(P, c.B, 3).contiguous()
+    loss = torch.empty(P, c.B, dtype=torch.float32, device=c.device)
+    L = N.lib()
+    nbytes = L.dpft_residual_poses_workspace_size(ctypes.byref(c.desc), P)
+    if nbytes == 0:
+        N.check(-1, "dpft_residual_poses_workspace_size")
+    ws = _workspace(c.device, nbytes)
+    rc = L.dpft_ic_residual_poses(ctypes.byref(c.desc), ctypes.byref(c.tens), P, _ptr(Rb), _ptr(tb), _ptr(loss),
+                                  _ptr(ws), nbytes, _stream(c.device))
+    N.check(rc, "dpft_ic_residual_poses")
+    return loss
+
+
 def debug_pixels(pose, x0, x1, invD0, invD1, K, sigma0, sigma1, **kw):
     """Per-pixel dump [B,5,H,W] (u, v, sigma_r ch0, sigma0 ch0, occlusion|mask invalid) -- tests only."""
     c = LevelCall(x0, x1, invD0, invD1, K, sigma0, sigma1, iters=1, **kw)

@@ -1,48 +1,61 @@
-"""Pose-error metrics used to report "3DPE vs ref" (host-side, PyTorch).
+"""Pose-error metrics of the evaluation scripts ("3DPE vs ref", RPE).
 
-Restated from the reference's criterions (code/models/criterions.py):
-3D end-point error = mean over valid reference pixels of
-|(R_a X + t_a) - (R_b X + t_b)|_2 with X the back-projected frame-0 depth
-(`compute_RT_EPE_loss` + `EPE3D_loss`, criterions.py:23-46, 101-136), and the
-relative pose error = (rotation angle, translation norm) of T_b^-1-between
-(`compute_RPE_loss`, criterions.py:49-57, 79-98; geometry.py:125-144, 187-207).
+Restated from the reference's criterions (code/models/criterions.py), same names
+and conventions, evaluation (non-training) branch:
+  EPE3D_loss            criterions.py:23-46   per-sample mean |flow_gt - flow_est|_2
+                                              over pixels that are not NaN / invalid
+  RPE                   criterions.py:49-57   (rotation angle, |t|) of a relative pose
+  compute_RPE_loss      criterions.py:79-98   RPE of between(T_est -> T_gt)
+  compute_RT_EPE_loss   criterions.py:101-136 3D end-point error of the back-projected
+                                              frame-0 depth under T_est vs T_gt
+Host-side PyTorch (runs on whichever device the tensors are on).
 """
 import torch
 
-
-def back_project(depth, K):
-    """[B,1,H,W] depth, [B,4] K -> [B,3,H*W] points (geometry.batch_inverse_project)."""
-    B, _, H, W = depth.shape
-    fx, fy, cx, cy = (K[:, i].view(B, 1) for i in range(4))
-    u = torch.arange(W, dtype=depth.dtype, device=depth.device).repeat(H).view(1, -1)
-    v = torch.arange(H, dtype=depth.dtype, device=depth.device).repeat_interleave(W).view(1, -1)
-    z = depth.reshape(B, -1)
-    return torch.stack(((u - cx) / fx * z, (v - cy) / fy * z, z), 1)
+from .models import geometry as geo
 
 
-def epe3d_between(Ra, ta, Rb, tb, depth, K, invalid=None):
-    """Per-pair mean 3D end-point error [B] between poses a and b."""
-    B = Ra.shape[0]
-    X = back_project(depth, K)
-    pa = torch.bmm(Ra, X) + ta.reshape(B, 3, 1)
-    pb = torch.bmm(Rb, X) + tb.reshape(B, 3, 1)
-    err = (pa - pb).norm(dim=1)
-    bad = torch.isnan(pb).any(1)
+def EPE3D_loss(input_flow, target_flow, invalid=None):
+    epe_map = torch.norm(target_flow - input_flow, p=2, dim=1)
+    B = epe_map.shape[0]
+    bad = torch.isnan(target_flow).any(1)
     if invalid is not None:
-        bad = bad | invalid.reshape(B, -1)
+        bad = bad | (invalid.view(bad.shape) > 0)
     out = []
     for i in range(B):
-        e = err[i][~bad[i]]
-        out.append(e.mean() if e.numel() else torch.zeros((), dtype=err.dtype, device=err.device))
+        e = epe_map[i][~bad[i]]
+        out.append(e.mean() if e.numel() else torch.zeros((), dtype=input_flow.dtype, device=input_flow.device))
     return torch.stack(out)
 
 
+def RPE(R, t):
+    return geo.batch_mat2angle(R), torch.norm(t.reshape(t.shape[0], 3), p=2, dim=1)
+
+
+def compute_RPE_loss(R_est, t_est, R_gt, t_gt):
+    dR, dt = geo.batch_Rt_between(R_est, t_est, R_gt, t_gt)
+    return RPE(dR, dt)
+
+
+def compute_RT_EPE_loss(R_est, t_est, R_gt, t_gt, depth0, K, invalid=None):
+    xyz = geo.batch_inverse_project(depth0, K)
+    flow_gt = geo.batch_transform_xyz(xyz, R_gt, t_gt)
+    flow_est = geo.batch_transform_xyz(xyz, R_est, t_est)
+    return EPE3D_loss(flow_est, flow_gt, invalid=invalid)
+
+
+# ---------------------------------------------------------------- bench helpers
+def back_project(depth, K):
+    """[B,1,H,W] depth, [B,4] K -> [B,3,H*W] points."""
+    B = depth.shape[0]
+    return geo.batch_inverse_project(depth, K).view(B, 3, -1)
+
+
+def epe3d_between(Ra, ta, Rb, tb, depth, K, invalid=None):
+    """Per-pair mean 3D end-point error [B] between poses a and b (compute_RT_EPE_loss)."""
+    return compute_RT_EPE_loss(Ra, ta, Rb, tb, depth, K, invalid=invalid)
+
+
 def rpe(Ra, ta, Rb, tb):
-    """(angle [B] rad, translation [B]) of the relative pose between a and b."""
-    B = Ra.shape[0]
-    dR = torch.bmm(Rb, Ra.transpose(1, 2))
-    dt = tb.reshape(B, 3) - torch.bmm(dR, ta.reshape(B, 3, 1)).view(B, 3)
-    tr = dR.diagonal(dim1=1, dim2=2).sum(1)
-    eps = 1e-7
-    ang = torch.acos(((tr - 1) / 2).clamp(-1 + eps, 1 - eps))
-    return ang, dt.norm(dim=1)
+    """(angle [B] rad, translation [B]) of the relative pose between a and b (compute_RPE_loss)."""
+    return compute_RPE_loss(Ra, ta, Rb, tb)

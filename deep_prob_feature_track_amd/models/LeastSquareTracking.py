@@ -23,6 +23,7 @@ import torch.nn as nn
 from .algorithms import (DeepRobustEstimator, DirectSolverNet, FeaturePyramid, ImagePyramids, PoseNet, ScaleNet,
                          SFMPoseNet, TrustRegionInverseWUncertainty)
 from .submodules import color_normalize
+from .. import ic
 
 # options attributes the reference constructor reads, with config.py's defaults
 DEFAULT_OPTIONS = dict(vis_feat=False, train_uncer_prop=False, combine_ICP=False, feature_extract='average',
@@ -158,6 +159,23 @@ class LeastSquareTracking(nn.Module):
             poseI, x0[i], x1[i], inv_d0[i], inv_d1[i], K / float(1 << i), sigma0=sigma0[i], sigma1=sigma1[i],
             wPrior=None, vis_res=False, depth0=dpt0[i], depth1=dpt1[i], obj_mask0=m0[i], obj_mask1=m1[i])
         return poseI, loss
+
+    def prepare(self, img0, img1, depth0, depth1, obj_mask0=None, obj_mask1=None):
+        """The preprocessed pyramids (`_preprocess` output) for reuse across many
+        residual evaluations -- the convergence-basin sweep computes them once
+        instead of once per pose (LeastSquareTracking.py:620)."""
+        return self._preprocess(img0, img1, depth0, depth1, poseI=None, obj_mask0=obj_mask0, obj_mask1=obj_mask1)
+
+    def compute_residual_poses(self, prepared, K, R, t, level_i=0):
+        """Losses [P,B] of P poses per pair at `level_i` in one launch: pose p is
+        what compute_residual(..., poseI=[R[p], t[p]], level_i) returns for the batch."""
+        (I0, I1, x0, x1, sigma0, sigma1, dpt0, dpt1, inv_d0, inv_d1, m0, m1, _) = prepared
+        i = level_i
+        tr = self.tr_update0
+        kw = tr._common(x0[i], dpt0[i], dpt1[i], m0[i], m1[i])
+        with torch.no_grad():
+            return ic.residual_poses(R, t, x0[i], x1[i], inv_d0[i], inv_d1[i], K / float(1 << i),
+                                     sigma0[i], sigma1[i], **kw)
 
     # ------------------------------------------------------------------ internals
     def _encode(self, img0, invD0, img1, invD1):

@@ -51,3 +51,41 @@ def batch_Rt_between(R0, t0, R1, t1):
     """Transform from T0 to T1: T1 T0^-1 = (R1 R0^T, t1 - R1 R0^T t0)."""
     dR = torch.bmm(R1, R0.transpose(1, 2))
     return dR, t1.reshape(-1, 3) - torch.bmm(dR, t0.reshape(-1, 3, 1)).view(-1, 3)
+
+
+def batch_mat2euler(M):
+    """Static x-y-z Euler angles (ax, ay, az) [B] each of rotations [B,3,3]
+    (geometry.py:506-554, 'sxyz': i, j, k = 0, 1, 2, no repetition / parity / frame)."""
+    cy = torch.sqrt(M[:, 0, 0] ** 2 + M[:, 1, 0] ** 2)
+    degenerate = ~(cy > 1e-8)
+    ax = torch.atan2(M[:, 2, 1], M[:, 2, 2])
+    ay = torch.atan2(-M[:, 2, 0], cy)
+    az = torch.atan2(M[:, 1, 0], M[:, 0, 0])
+    if bool(degenerate.any()):
+        ax = torch.where(degenerate, torch.atan2(-M[:, 1, 2], M[:, 1, 1]), ax)
+        az = torch.where(degenerate, torch.zeros_like(az), az)
+    return ax, ay, az
+
+
+def batch_mat2angle(R):
+    """Rotation angle [B] of rotations [B,3,3] (geometry.py:187-207)."""
+    tr = torch.stack([torch.trace(R[i]) for i in range(R.shape[0])])  # the reference's per-matrix trace
+    eps = 1e-7
+    return torch.acos(((tr - 1) / 2).clamp(-1 + eps, 1 - eps))
+
+
+def batch_inverse_project(depth, K):
+    """[B,1,H,W] depth, [B,4] K -> [B,3,H,W] camera points (geometry.py:429-445)."""
+    B, _, H, W = depth.shape
+    fx, fy, cx, cy = (K[:, i].view(B, 1, 1, 1) for i in range(4))
+    v, u = torch.meshgrid(torch.arange(H, dtype=depth.dtype, device=depth.device),
+                          torch.arange(W, dtype=depth.dtype, device=depth.device), indexing='ij')
+    x = (u.view(1, 1, H, W) - cx) / fx * depth
+    y = (v.view(1, 1, H, W) - cy) / fy * depth
+    return torch.cat((x, y, depth), 1)
+
+
+def batch_transform_xyz(xyz, R, t):
+    """R xyz + t for [B,3,H,W] points (geometry.py:376-399, without the Jacobian)."""
+    B, _, H, W = xyz.shape
+    return (torch.bmm(R, xyz.view(B, 3, -1)) + t.reshape(B, 3, 1)).view(B, 3, H, W)

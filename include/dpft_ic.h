@@ -124,6 +124,19 @@ int dpft_ic_residual_level(const DpftLevelDesc* desc, const DpftLevelTensors* te
                            const float* R, const float* t, float* loss,
                            void* workspace, size_t workspace_bytes, void* hip_stream);
 
+/*
+ * Residual-only evaluation of n_poses poses per pair in one launch (the
+ * convergence-basin sweep, convergence_basin.py:85-475, with the feature
+ * pyramid computed once instead of once per pose as LeastSquareTracking.py:620
+ * does).  R [n_poses,B,3,3], t [n_poses,B,3], loss [n_poses,B]; pose p is
+ * evaluated as one reference call over the batch (its own batch-global
+ * truncated-sigma extrema).  Workspace: dpft_residual_poses_workspace_size.
+ */
+size_t dpft_residual_poses_workspace_size(const DpftLevelDesc* desc, int32_t n_poses);
+int dpft_ic_residual_poses(const DpftLevelDesc* desc, const DpftLevelTensors* tensors, int32_t n_poses,
+                           const float* R, const float* t, float* loss,
+                           void* workspace, size_t workspace_bytes, void* hip_stream);
+
 /* Kernel-only timing hook for the roofline: launch ONLY the fused residual +
  * Jacobian + normal-equation kernel (no finalize), using the sigma0 extrema a
  * previous dpft_ic_iterate(first=1) left in the workspace.  Used by bench.py. */

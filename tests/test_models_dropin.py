@@ -98,3 +98,50 @@ def test_forward_and_residual_match_reference(name):
         _, loss2 = m.compute_residual(T["img0"], T["img1"], T["depth0"], T["depth1"], T["K"], poseI=ident,
                                       level_i=2, **kw)
         np.testing.assert_allclose(loss2.cpu().numpy(), z["res_init_loss"], rtol=1e-4)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("name", ["convrgbd2_c8", "convrgbd2_c8_icp", "rgb_identity_masks"])
+def test_convergence_basin_landscape_matches_reference(name):
+    """The multi-pose residual sweep equals the reference's one-compute_residual-per-pose
+    loop (convergence_basin.py:340-369, 405-426) at levels 0 and 1."""
+    from deep_prob_feature_track_amd import convergence_basin as CB
+    m, T = _loaded(name, "cuda")
+    z = np.load(os.path.join(HERE, f"model_{name}.npz"), allow_pickle=False)
+    R_gt = torch.from_numpy(z["R"]).cuda()
+    B = R_gt.shape[0]
+    t_gt = torch.from_numpy(z["t"]).cuda().view(B, 3)
+    offs = list(z["basin_offsets"])
+    kw = dict(obj_mask0=T.get("mask0"), obj_mask1=T.get("mask1"))
+    prep = m.prepare(T["img0"], T["img1"], T["depth0"], T["depth1"], **kw)
+    Rp, tp = CB.axis_perturbations(R_gt, t_gt, offs, offs)
+    for li, level in enumerate((0, 1)):
+        got = m.compute_residual_poses(prep, T["K"], Rp, tp, level_i=level).view(6, len(offs), B).cpu().numpy()
+        np.testing.assert_allclose(got, z["basin_loss"][li], rtol=1e-3)
+
+
+@pytest.mark.gpu
+def test_convergence_basin_driver_outputs():
+    from deep_prob_feature_track_amd import convergence_basin as CB
+    m, T = _loaded("convrgbd2_c8", "cuda")
+    z = np.load(os.path.join(HERE, "model_convrgbd2_c8.npz"), allow_pickle=False)
+    B = z["R"].shape[0]
+    Rt = torch.eye(4).repeat(B, 1, 1).cuda()
+    Rt[:, :3, :3] = torch.from_numpy(z["R"]).cuda()
+    Rt[:, :3, 3] = torch.from_numpy(z["t"]).cuda().view(B, 3)
+    S = 5
+    out = CB.evaluate_convergence_basin(m, T["img0"], T["img1"], T["depth0"], T["depth1"], Rt, T["K"],
+                                        level_i=[0, 1], pert_samples=S)
+    assert out["avg_loss"].shape == (6, S + 3, B) and out["coarse_avg_loss"].shape == (1, 6, S, B)
+    # the zero offset of every axis is the ground truth itself (= the reference's forward pose)
+    for i in range(6):
+        np.testing.assert_allclose(out["avg_loss"][i, S // 2], z["res_pose_loss"], rtol=1e-3)
+    # the optimised pose (our forward) sits at the bottom of the basin as the reference's does
+    np.testing.assert_allclose(out["avg_loss"][0, S + 2], z["res_pose_loss"], rtol=1e-3)
+    assert np.all(out["angular_error"] < 1e-3) and np.all(out["translation_error"] < 1e-3)
+    n, margins = CB.convergence_counts(torch.from_numpy(out["R_est"]), torch.from_numpy(out["t_est"]),
+                                       torch.from_numpy(z["R"]), torch.from_numpy(z["t"]).view(B, 3))
+    assert n == B and np.all(margins["rot_margin"] > 0)
+    d2 = CB.evaluate_2d_convergence_basin(m, T["img0"], T["img1"], T["depth0"], T["depth1"], Rt, T["K"],
+                                          pert_samples=3)
+    np.testing.assert_allclose(d2["avg_loss"][0, 1, 1], z["res_pose_loss"], rtol=1e-3)
