@@ -38,7 +38,8 @@ class LevelTensors(ctypes.Structure):
 
 EXPORTS = ("dpft_workspace_size", "dpft_ic_solve_level", "dpft_ic_iterate", "dpft_ic_residual_level",
            "dpft_residual_poses_workspace_size", "dpft_ic_residual_poses",
-           "dpft_ic_reduce_only", "dpft_ic_debug_pixels", "dpft_version", "dpft_last_error")
+           "dpft_ic_reduce_only", "dpft_ic_debug_pixels", "dpft_preprocess_workspace_size",
+           "dpft_preprocess_depth", "dpft_version", "dpft_last_error")
 
 _lib = None
 
@@ -69,6 +70,11 @@ def lib():
     L.dpft_ic_reduce_only.restype = ctypes.c_int
     L.dpft_ic_debug_pixels.argtypes = [P(LevelDesc), P(LevelTensors), vp, vp, vp, vp, sz, vp]
     L.dpft_ic_debug_pixels.restype = ctypes.c_int
+    L.dpft_preprocess_workspace_size.argtypes = []
+    L.dpft_preprocess_workspace_size.restype = sz
+    L.dpft_preprocess_depth.argtypes = [vp, ctypes.c_int32, ctypes.c_int32, ctypes.c_int32, ctypes.c_int32,
+                                        P(vp), P(vp), vp, sz, vp]
+    L.dpft_preprocess_depth.restype = ctypes.c_int
     L.dpft_version.argtypes = []
     L.dpft_version.restype = ctypes.c_int
     L.dpft_last_error.argtypes = []

@@ -1493,6 +1493,95 @@ __global__ __launch_bounds__(kThreads) void minmax_kernel(const float* __restric
   }
 }
 
+// ============================================================ depth preprocessing
+// LeastSquareTracking._preprocess (LeastSquareTracking.py:653-661, 669-670):
+// invD = clamp(1 / depth, 0, 10); zero the batch-global min, then the max;
+// ImagePyramids(pool='max') (algorithms.py:1201-1219) of invD (and of the raw
+// depth for ICP).  Bit-exact: IEEE division, NaN-propagating clamp and max.
+__device__ __forceinline__ float invd_of(float d) {
+  const float x = 1.0f / d;
+  return x < 0.0f ? 0.0f : (x > 10.0f ? 10.0f : x);  // torch.clamp (NaN stays NaN)
+}
+
+__global__ __launch_bounds__(kThreads) void invd_minmax_kernel(const float* __restrict__ depth, size_t n,
+                                                               uint32_t* ctrl) {
+  __shared__ float sm[2][4];
+  float mn = INFINITY, mx = -INFINITY;
+  const size_t stride = (size_t)gridDim.x * kThreads;
+  for (size_t i = (size_t)blockIdx.x * kThreads + threadIdx.x; i < n; i += stride) {
+    const float v = invd_of(depth[i]);
+    mn = fminf(mn, v);
+    mx = fmaxf(mx, v);
+  }
+  for (int off = 32; off > 0; off >>= 1) {
+    mn = fminf(mn, __shfl_xor(mn, off));
+    mx = fmaxf(mx, __shfl_xor(mx, off));
+  }
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  if (lane == 0) {
+    sm[0][wave] = mn;
+    sm[1][wave] = mx;
+  }
+  __syncthreads();
+  float* part = reinterpret_cast<float*>(ctrl + kCtlPart);
+  if (threadIdx.x == 0) {
+    st_ag(part + 2 * blockIdx.x, fminf(fminf(sm[0][0], sm[0][1]), fminf(sm[0][2], sm[0][3])));
+    st_ag(part + 2 * blockIdx.x + 1, fmaxf(fmaxf(sm[1][0], sm[1][1]), fmaxf(sm[1][2], sm[1][3])));
+  }
+  if (!block_is_last(ctrl + kCtlMMDone, 1u, gridDim.x)) return;
+  if (threadIdx.x < 64) {
+    mn = INFINITY;
+    mx = -INFINITY;
+    for (int k = threadIdx.x; k < (int)gridDim.x; k += 64) {
+      mn = fminf(mn, ld_ag(part + 2 * k));
+      mx = fmaxf(mx, ld_ag(part + 2 * k + 1));
+    }
+    for (int off = 32; off > 0; off >>= 1) {
+      mn = fminf(mn, __shfl_xor(mn, off));
+      mx = fmaxf(mx, __shfl_xor(mx, off));
+    }
+    if (threadIdx.x == 0) {
+      // the max is taken after the min pixels were zeroed (LeastSquareTracking.py:658-661)
+      const float mx2 = (mx == mn) ? 0.0f : mx;
+      ctrl[kCtlMin] = enc_ord(mn);
+      ctrl[kCtlMax] = enc_ord(mx2);
+    }
+  }
+}
+
+struct PyrOut {
+  float* invd[4];
+  float* depth[4];
+};
+
+// blockIdx.y = level l: each thread writes one level-l pixel, the max over its
+// 2^l x 2^l block (MaxPool2d(2^l, 2^l): floor-sized output, remainder ignored).
+__global__ __launch_bounds__(kThreads) void invd_pyramid_kernel(const float* __restrict__ depth, int B, int H, int W,
+                                                                const uint32_t* __restrict__ ctrl, PyrOut out) {
+  const int l = blockIdx.y, k = 1 << l;
+  const int Hl = H / k, Wl = W / k;
+  const long i = (long)blockIdx.x * kThreads + threadIdx.x;
+  if (i >= (long)B * Hl * Wl) return;
+  const int b = (int)(i / ((long)Hl * Wl)), rem = (int)(i - (long)b * Hl * Wl), y = rem / Wl, x = rem - y * Wl;
+  const float gmin = dec_ord(ctrl[kCtlMin]), gmax = dec_ord(ctrl[kCtlMax]);
+  const float* db = depth + (size_t)b * H * W;
+  float mi = -INFINITY, md = -INFINITY;
+  bool nan_i = false, nan_d = false;
+  for (int yy = y * k; yy < y * k + k; ++yy)
+    for (int xx = x * k; xx < x * k + k; ++xx) {
+      const float d = db[yy * W + xx];
+      float v = invd_of(d);
+      if (v == gmin || v == gmax) v = 0.0f;
+      nan_i |= v != v;
+      nan_d |= d != d;
+      mi = fmaxf(mi, v);
+      md = fmaxf(md, d);
+    }
+  const size_t o = (size_t)b * Hl * Wl + rem;
+  out.invd[l][o] = nan_i ? NAN : mi;
+  if (out.depth[l]) out.depth[l][o] = nan_d ? NAN : md;
+}
+
 // ------------------------------------------------------------------ host side
 struct Geometry {
   int tiles_x, tiles_y, steps, nblocks, per_pair;
@@ -1825,6 +1914,32 @@ int dpft_ic_debug_pixels(const DpftLevelDesc* desc, const DpftLevelTensors* tt, 
   hipLaunchKernelGGL(ic_debug_pixels_kernel, dim3((n + kThreads - 1) / kThreads), dim3(kThreads), 0,
                      static_cast<hipStream_t>(hip_stream), p, out);
   return hip_check("ic_debug_pixels_kernel");
+}
+
+size_t dpft_preprocess_workspace_size(void) { return kCtrlBytes; }
+
+int dpft_preprocess_depth(const float* depth, int32_t B, int32_t H, int32_t W, int32_t levels, float* const* invd_out,
+                          float* const* depth_out, void* ws, size_t ws_bytes, void* hip_stream) {
+  if (!depth || !invd_out || !ws) return fail(DPFT_E_INVALID, "null pointer");
+  if (B < 1 || H < 1 || W < 1 || levels < 1 || levels > 4 || (H >> (levels - 1)) < 1 || (W >> (levels - 1)) < 1)
+    return fail(DPFT_E_INVALID, "bad shape B=%d H=%d W=%d levels=%d", B, H, W, levels);
+  if (ws_bytes < kCtrlBytes) return fail(DPFT_E_WORKSPACE, "workspace %zu < %zu", ws_bytes, kCtrlBytes);
+  PyrOut out;
+  for (int l = 0; l < 4; ++l) {
+    out.invd[l] = l < levels ? invd_out[l] : nullptr;
+    out.depth[l] = (l < levels && depth_out) ? depth_out[l] : nullptr;
+    if (l < levels && !out.invd[l]) return fail(DPFT_E_INVALID, "null invD output of level %d", l);
+  }
+  hipStream_t st = static_cast<hipStream_t>(hip_stream);
+  uint32_t* ctrl = static_cast<uint32_t*>(ws);
+  const size_t n = (size_t)B * H * W;
+  const int grid = (int)std::min<size_t>((n + kThreads * 16 - 1) / (kThreads * 16), kMaxMMBlocks);
+  hipLaunchKernelGGL(invd_minmax_kernel, dim3(grid), dim3(kThreads), 0, st, depth, n, ctrl);
+  int rc = hip_check("invd_minmax_kernel");
+  if (rc) return rc;
+  hipLaunchKernelGGL(invd_pyramid_kernel, dim3((unsigned)((n + kThreads - 1) / kThreads), levels), dim3(kThreads), 0,
+                     st, depth, B, H, W, ctrl, out);
+  return hip_check("invd_pyramid_kernel");
 }
 
 int dpft_version(void) { return DPFT_ABI_VERSION; }

@@ -174,6 +174,28 @@ def residual_poses(R, t, x0, x1, invD0, invD1, K, sigma0, sigma1, **kw):
     return loss
 
 
+def preprocess_depth(depth, levels=4, depth_pyramid=False):
+    """LeastSquareTracking._preprocess on the device: invD = clamp(1/depth, 0, 10) with the
+    batch-global min then max zeroed, and MaxPool(2^l) pyramids of invD (and of depth).
+    depth [B,1,H,W] fp32 on a HIP device -> ([invD_l], [depth_l] or None)."""
+    if not depth.is_cuda:
+        raise RuntimeError("preprocess_depth needs a device tensor; there is no CPU fallback")
+    if depth.dtype != torch.float32 or depth.dim() != 4 or depth.shape[1] != 1:
+        raise ValueError(f"depth must be fp32 [B,1,H,W], got {depth.dtype} {tuple(depth.shape)}")
+    d = depth.contiguous()
+    B, _, H, W = d.shape
+    inv = [torch.empty(B, 1, H >> l, W >> l, dtype=torch.float32, device=d.device) for l in range(levels)]
+    dep = [torch.empty_like(t) for t in inv] if depth_pyramid else None
+    arr = (ctypes.c_void_p * levels)(*[t.data_ptr() for t in inv])
+    darr = (ctypes.c_void_p * levels)(*[t.data_ptr() for t in dep]) if dep else None
+    L = N.lib()
+    nbytes = L.dpft_preprocess_workspace_size()
+    ws = _workspace(d.device, nbytes)
+    rc = L.dpft_preprocess_depth(_ptr(d), B, H, W, levels, arr, darr, _ptr(ws), nbytes, _stream(d.device))
+    N.check(rc, "dpft_preprocess_depth")
+    return inv, dep
+
+
 def debug_pixels(pose, x0, x1, invD0, invD1, K, sigma0, sigma1, **kw):
     """Per-pixel dump [B,5,H,W] (u, v, sigma_r ch0, sigma0 ch0, occlusion|mask invalid) -- tests only."""
     c = LevelCall(x0, x1, invD0, invD1, K, sigma0, sigma1, iters=1, **kw)

@@ -198,18 +198,24 @@ class LeastSquareTracking(nn.Module):
 
     def _preprocess(self, img0, img1, depth0, depth1, poseI=None, obj_mask0=None, obj_mask1=None):
         """LeastSquareTracking.py:653-699."""
-        invD0 = self._inverse_depth(depth0)
-        invD1 = self._inverse_depth(depth1)
+        if depth0.is_cuda:  # fused device pre-pass (dpft_preprocess_depth), bit-identical to the torch ops
+            inv_d0, dp0 = ic.preprocess_depth(depth0, len(self.scales), depth_pyramid=self.combine_icp)
+            inv_d1, dp1 = ic.preprocess_depth(depth1, len(self.scales), depth_pyramid=self.combine_icp)
+            invD0, invD1 = inv_d0[0], inv_d1[0]
+        else:
+            invD0 = self._inverse_depth(depth0)
+            invD1 = self._inverse_depth(depth1)
+            inv_d0 = self.construct_depth_pyramids(invD0)
+            inv_d1 = self.construct_depth_pyramids(invD1)
+            dp0 = dp1 = None
         I0 = color_normalize(img0)
         I1 = color_normalize(img1)
         with torch.no_grad():
             x0, sigma0, orig_x0 = self._encode(I0, invD0, I1, invD1)
             x1, sigma1, orig_x1 = self._encode(I1, invD1, I0, invD0)
-        inv_d0 = self.construct_depth_pyramids(invD0)
-        inv_d1 = self.construct_depth_pyramids(invD1)
         if self.combine_icp:
-            dpt0 = self.construct_depth_pyramids(depth0)
-            dpt1 = self.construct_depth_pyramids(depth1)
+            dpt0 = dp0 if dp0 is not None else self.construct_depth_pyramids(depth0)
+            dpt1 = dp1 if dp1 is not None else self.construct_depth_pyramids(depth1)
         else:
             dpt0 = dpt1 = [None] * len(self.scales)
         m0 = self.construct_image_pyramids(obj_mask0) if obj_mask0 is not None else [None] * len(self.scales)

@@ -150,6 +150,20 @@ int dpft_ic_debug_pixels(const DpftLevelDesc* desc, const DpftLevelTensors* tens
                          const float* R, const float* t, float* out,
                          void* workspace, size_t workspace_bytes, void* hip_stream);
 
+/*
+ * Depth preprocessing of LeastSquareTracking._preprocess (LeastSquareTracking.py:
+ * 653-661, 669-676): invD = clamp(1/depth, 0, 10) with the batch-global min and
+ * then max zeroed, and the max-pool pyramids (algorithms.py:1201-1219) of invD
+ * and (depth_out non-NULL, for ICP) of the raw depth.  depth [B,1,H,W];
+ * invd_out / depth_out: host arrays of `levels` device pointers, level l is
+ * [B,1,H>>l,W>>l].  Workspace: dpft_preprocess_workspace_size() bytes, zero-filled
+ * once (shared with the solver's workspace is fine on the same stream).
+ */
+size_t dpft_preprocess_workspace_size(void);
+int dpft_preprocess_depth(const float* depth, int32_t B, int32_t H, int32_t W, int32_t levels,
+                          float* const* invd_out, float* const* depth_out,
+                          void* workspace, size_t workspace_bytes, void* hip_stream);
+
 int dpft_version(void);            /* DPFT_ABI_VERSION */
 const char* dpft_last_error(void); /* thread-local message of the last failure */
 

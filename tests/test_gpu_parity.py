@@ -255,3 +255,26 @@ def test_hip_icp_matches_oracle_random(B, C, Cs, H, W, tru, masks):
         dR = (Rg.cpu() - ref["R"]).abs().max().item()
         dt = (tg.view(B, 3).cpu() - ref["t"]).abs().max().item()
         assert dR <= SE3_TOL and dt <= SE3_TOL, f"iter {it}: |dR|={dR:.2e} |dt|={dt:.2e}"
+
+
+@pytest.mark.parametrize("B,H,W,levels,extreme", [(2, 120, 160, 4, False), (3, 37, 70, 3, True), (1, 8, 8, 4, True)])
+def test_preprocess_depth_bit_exact(B, H, W, levels, extreme):
+    """dpft_preprocess_depth == the reference's torch ops (LeastSquareTracking.py:656-661, ImagePyramids max)."""
+    import torch.nn.functional as F
+    from deep_prob_feature_track_amd import ic
+    dev = _dev()
+    g = torch.Generator().manual_seed(B * 100 + H)
+    depth = 0.3 + 6.0 * torch.rand(B, 1, H, W, generator=g)
+    if extreme:
+        depth[0, 0, 0, :3] = 0.0          # 1/0 -> inf -> clamped to 10 (the max)
+        depth[-1, 0, -1, -2:] = 200.0     # tiny inverse depth (the min)
+    ref = torch.clamp(1.0 / depth, 0, 10)
+    ref[ref == ref.min()] = 0
+    ref[ref == ref.max()] = 0
+    inv, dep = ic.preprocess_depth(depth.to(dev), levels, depth_pyramid=True)
+    for l in range(levels):
+        k = 1 << l
+        want = F.max_pool2d(ref, k, k) if k > 1 else ref
+        wantd = F.max_pool2d(depth, k, k) if k > 1 else depth
+        assert torch.equal(inv[l].cpu(), want), f"invD level {l}"
+        assert torch.equal(dep[l].cpu(), wantd), f"depth level {l}"
