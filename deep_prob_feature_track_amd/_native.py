@@ -15,6 +15,7 @@ LIB_PATH = os.path.join(_HERE, "libdpft_ic.so")
 
 REMOVE_TRU_SIGMA = 0x1
 COMBINE_ICP = 0x2
+NO_UNCERTAINTY = 0x4
 STATUS_NONFINITE = 0x1
 ABI_VERSION = 1
 

@@ -977,8 +977,13 @@ __device__ void finalize_loss(const FinParams& q) {
 // prologue / epilogue per workgroup, and consecutive tiles are vertically
 // adjacent, so the halo rows of f0 / sigma0 are re-read from L2 right after
 // their first use.  Workgroup k writes record slot k.
-template <int CT, bool CS1, bool TRU, bool ICP>
+// MODE: 0 = U_IC (TrustRegionInverseWUncertainty), 1 = U_IC + combine_ICP,
+//       2 = IC without uncertainty (TrustRegionBase, algorithms.py:23-139: sigma = 1,
+//           J = Jf_x Jx + Jf_y Jy (1867-1882), occluded residual 1e-3 (1955)).
+template <int CT, bool CS1, bool TRU, int MODE>
 __global__ __launch_bounds__(kThreads, DPFT_MIN_WAVES) void ic_reduce_kernel(IterParams p) {
+  constexpr bool ICP = MODE == 1, NOSIG = MODE == 2;
+  constexpr float kFill = NOSIG ? 1e-3f : 1e-6f;  // weighted residual of invalid pixels
   const int C = CT > 0 ? CT : p.C;
   __shared__ float lds_ext[TRU ? 2 * 7 : 1][kThreads];  // extremum corrections (6 + count), min then max
   __shared__ float red[4][kRec];
@@ -1069,7 +1074,7 @@ __global__ __launch_bounds__(kThreads, DPFT_MIN_WAVES) void ic_reduce_kernel(Ite
     const float m1 = m1b ? bil_u8(m1b, tp) : 1.0f;
     float s0t = 0.f, s0m = 0.f, s0b_ = 0.f;
     Gather4 gs1;
-    if (CS1) {
+    if (CS1 && !NOSIG) {
       s0t = bld(rs0, colv, rT);
       s0m = bld(rs0, colv, rM);
       s0b_ = bld(rs0, colv, rB);
@@ -1100,8 +1105,8 @@ __global__ __launch_bounds__(kThreads, DPFT_MIN_WAVES) void ic_reduce_kernel(Ite
                       (wp.v < (float)H);
       invalid = !ok || !out_lane || !m0 || !(m1 > 0.0f);
     }
-    float sr0 = 0.f, srmin = 0.f, srmax = 0.f, inv_s = 0.f, kk = 0.f, hx = 0.f, hy = 0.f;
-    if (CS1) {
+    float sr0 = 0.f, srmin = 0.f, srmax = 0.f, inv_s = NOSIG ? 1.0f : 0.f, kk = 0.f, hx = 0.f, hy = 0.f;
+    if (CS1 && !NOSIG) {
       sobel_cols(s0t, s0m, s0b_, hx, hy);
       sr0 = bilp(gs1, pw);
       srmin = srmax = sr0;
@@ -1122,7 +1127,7 @@ __global__ __launch_bounds__(kThreads, DPFT_MIN_WAVES) void ic_reduce_kernel(Ite
         sobel_cols(cur[cc].t, cur[cc].m, cur[cc].b, gx, gy);
         const float f0v = cur[cc].m;
         float is_c = inv_s, kk_c = kk, hx_c = hx, hy_c = hy;
-        if (!CS1) {
+        if (!CS1 && !NOSIG) {
           const int po = c * (int)planeB;
           const float st_ = bld(rs0, colv, po + rT), sm_ = bld(rs0, colv, po + rM), sb_ = bld(rs0, colv, po + rB);
           sobel_cols(st_, sm_, sb_, hx_c, hy_c);
@@ -1170,8 +1175,8 @@ __global__ __launch_bounds__(kThreads, DPFT_MIN_WAVES) void ic_reduce_kernel(Ite
       float Jx[6], Jy[6];
       warp_jac(wp.xr, wp.yr, d, fx, fy, Jx, Jy);
       // weighted residual of invalid pixels is 1e-6 on every channel (algorithms.py:1982-1983)
-      const float cA = invalid ? 1e-6f * Sa : Sar;
-      const float cB = invalid ? 1e-6f * Sb : Sbr;
+      const float cA = invalid ? kFill * Sa : Sar;
+      const float cB = invalid ? kFill * Sb : Sbr;
       float P[6], Q[6];
 #pragma unroll
       for (int i = 0; i < 6; ++i) {
@@ -1312,8 +1317,9 @@ __global__ __launch_bounds__(kThreads, DPFT_MIN_WAVES) void ic_reduce_kernel(Ite
 // blockIdx.y = pose index: P poses per pair share the level's inputs; pose p
 // evaluates the batch of B pairs at R[p], t[p] (its own batch-global
 // truncated-sigma extrema, as one reference call per pose would).
-template <bool CS1, bool ICP>
+template <bool CS1, int MODE>
 __global__ __launch_bounds__(kThreads) void ic_residual_kernel(IterParams p) {
+  constexpr bool ICP = MODE == 1, NOSIG = MODE == 2;
   __shared__ float red[4][16];
   const int tid = threadIdx.x, lane = tid & 63, wave = wave_id();
   const int bid = xcd_remap(blockIdx.x, p.nblocks);
@@ -1345,6 +1351,11 @@ __global__ __launch_bounds__(kThreads) void ic_residual_kernel(IterParams p) {
     setup_pixel(p, b, x, y, p.invD0[(size_t)b * HW + pix], Rm, tv, fx, fy, cx, cy, px);
     float srr = 0.f, smin = INFINITY, smax = -INFINITY, sr0 = 0.f, s00 = 0.f;
     for (int c = 0; c < C; ++c) {
+      if (NOSIG) {  // TrustRegionBase.forward_residuals: r = f1(warp) - f0 (algorithms.py:1919-1957)
+        const float r = bil(f1b + (size_t)c * HW, px.tp) - f0b[(size_t)c * HW + pix];
+        srr += r * r;
+        continue;
+      }
       const int cs = CS1 ? 0 : c;
       const float s0c = s0b[(size_t)cs * HW + pix];
       const float src = bil(s1b + (size_t)cs * HW, px.tp);
@@ -1610,12 +1621,15 @@ int check_desc(const DpftLevelDesc* d) {
   if (d->B > kMaxPairs) return fail(DPFT_E_INVALID, "B=%d exceeds %d pairs per call", d->B, kMaxPairs);
   if ((d->flags & DPFT_COMBINE_ICP) && !(d->icp_weight == d->icp_weight))
     return fail(DPFT_E_INVALID, "icp_weight is NaN");
+  if ((d->flags & DPFT_NO_UNCERTAINTY) && (d->flags & (DPFT_REMOVE_TRU_SIGMA | DPFT_COMBINE_ICP)))
+    return fail(DPFT_E_INVALID, "NO_UNCERTAINTY (IC tracker) excludes REMOVE_TRU_SIGMA and COMBINE_ICP");
   return DPFT_OK;
 }
 
 int check_tensors(const DpftLevelTensors* t, uint32_t flags = 0) {
-  if (!t || !t->f0 || !t->f1 || !t->s0 || !t->s1 || !t->invD0 || !t->invD1 || !t->K)
+  if (!t || !t->f0 || !t->f1 || !t->invD0 || !t->invD1 || !t->K)
     return fail(DPFT_E_INVALID, "null tensor pointer");
+  if (!(flags & DPFT_NO_UNCERTAINTY) && (!t->s0 || !t->s1)) return fail(DPFT_E_INVALID, "null sigma pointer");
   if ((flags & DPFT_COMBINE_ICP) && (!t->depth0 || !t->depth1))
     return fail(DPFT_E_INVALID, "COMBINE_ICP needs depth0 and depth1");
   return DPFT_OK;
@@ -1753,27 +1767,31 @@ int resident_blocks(const void* kernel) {
   return n;
 }
 
-template <int CT, bool CS1, bool TRU, bool ICP>
+template <int CT, bool CS1, bool TRU, int MODE>
 int launch_reduce_k(IterParams p, hipStream_t st) {
-  const void* k = reinterpret_cast<const void*>(&ic_reduce_kernel<CT, CS1, TRU, ICP>);
+  const void* k = reinterpret_cast<const void*>(&ic_reduce_kernel<CT, CS1, TRU, MODE>);
   const int cap = resident_blocks(k);
   if (cap <= 0) return fail(DPFT_E_HIP, "occupancy query failed");
   p.nbpp = std::max(1, std::min(cap / p.B, p.per_pair));
   p.fin.nbpp = p.nbpp;
-  hipLaunchKernelGGL((ic_reduce_kernel<CT, CS1, TRU, ICP>), dim3(p.B * p.nbpp), dim3(kThreads), 0, st, p);
+  hipLaunchKernelGGL((ic_reduce_kernel<CT, CS1, TRU, MODE>), dim3(p.B * p.nbpp), dim3(kThreads), 0, st, p);
   return DPFT_OK;
 }
 
 template <int CT, bool CS1>
 int launch_reduce_t(const IterParams& p, hipStream_t st) {
   const bool tru = (p.flags & DPFT_REMOVE_TRU_SIGMA) != 0;
+  if (p.flags & DPFT_NO_UNCERTAINTY) {
+    if constexpr (CS1) return launch_reduce_k<CT, true, false, 2>(p, st);
+    else return fail(DPFT_E_INVALID, "internal: no IC instantiation for Cs=C");
+  }
   if (p.flags & DPFT_COMBINE_ICP) {
     if constexpr (CS1 || CT == 0)
-      return tru ? launch_reduce_k<CT, CS1, true, true>(p, st) : launch_reduce_k<CT, CS1, false, true>(p, st);
+      return tru ? launch_reduce_k<CT, CS1, true, 1>(p, st) : launch_reduce_k<CT, CS1, false, 1>(p, st);
     else
       return fail(DPFT_E_INVALID, "internal: no ICP instantiation for C=%d, Cs=C", CT);
   }
-  return tru ? launch_reduce_k<CT, CS1, true, false>(p, st) : launch_reduce_k<CT, CS1, false, false>(p, st);
+  return tru ? launch_reduce_k<CT, CS1, true, 0>(p, st) : launch_reduce_k<CT, CS1, false, 0>(p, st);
 }
 
 int launch_reduce(const IterParams& p, hipStream_t st) {
@@ -1834,16 +1852,18 @@ int residual_impl(const DpftLevelDesc* desc, const DpftLevelTensors* tt, int P, 
   p.fin.loss_out = loss;
   const dim3 grid(p.nblocks, P);
   const bool icp = (desc->flags & DPFT_COMBINE_ICP) != 0;
-  if (p.Cs == 1) {
+  if (desc->flags & DPFT_NO_UNCERTAINTY)
+    hipLaunchKernelGGL((ic_residual_kernel<true, 2>), grid, dim3(kThreads), 0, st, p);
+  else if (p.Cs == 1) {
     if (icp)
-      hipLaunchKernelGGL((ic_residual_kernel<true, true>), grid, dim3(kThreads), 0, st, p);
+      hipLaunchKernelGGL((ic_residual_kernel<true, 1>), grid, dim3(kThreads), 0, st, p);
     else
-      hipLaunchKernelGGL((ic_residual_kernel<true, false>), grid, dim3(kThreads), 0, st, p);
+      hipLaunchKernelGGL((ic_residual_kernel<true, 0>), grid, dim3(kThreads), 0, st, p);
   } else {
     if (icp)
-      hipLaunchKernelGGL((ic_residual_kernel<false, true>), grid, dim3(kThreads), 0, st, p);
+      hipLaunchKernelGGL((ic_residual_kernel<false, 1>), grid, dim3(kThreads), 0, st, p);
     else
-      hipLaunchKernelGGL((ic_residual_kernel<false, false>), grid, dim3(kThreads), 0, st, p);
+      hipLaunchKernelGGL((ic_residual_kernel<false, 0>), grid, dim3(kThreads), 0, st, p);
   }
   return hip_check("ic_residual_kernel");
 }

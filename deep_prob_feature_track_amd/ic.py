@@ -57,7 +57,7 @@ class LevelCall:
 
     def __init__(self, x0, x1, invD0, invD1, K, sigma0, sigma1, iters=3, remove_tru_sigma=False,
                  obj_mask0=None, obj_mask1=None, depth0=None, depth1=None, combine_icp=False,
-                 icp_weight=0.01, status=None):
+                 icp_weight=0.01, status=None, no_uncertainty=False):
         if not x0.is_cuda:
             raise RuntimeError("the HIP solver needs device tensors (got CPU); there is no CPU fallback")
         for name, t in (("x0", x0), ("x1", x1), ("invD0", invD0), ("invD1", invD1), ("K", K)):
@@ -73,15 +73,22 @@ class LevelCall:
                 raise ValueError(f"{name} shape {tuple(t.shape)} != {(B, 1, H, W)}")
         self.device = x0.device
         self.x0, self.x1 = x0.contiguous(), x1.contiguous()
-        self.s0, cs0 = _sigma_planes(sigma0, B, C, H, W)
-        self.s1, cs1 = _sigma_planes(sigma1, B, C, H, W)
-        if cs0 != cs1:  # mixed layouts: fall back to full planes for both
-            self.s0, self.s1, cs0 = sigma0.expand(B, C, H, W).contiguous(), sigma1.expand(B, C, H, W).contiguous(), C
+        if no_uncertainty:  # IC tracker (TrustRegionBase): sigma = 1, no sigma planes
+            self.s0 = self.s1 = None
+            cs0 = 1
+        else:
+            self.s0, cs0 = _sigma_planes(sigma0, B, C, H, W)
+            self.s1, cs1 = _sigma_planes(sigma1, B, C, H, W)
+            if cs0 != cs1:  # mixed layouts: full planes for both
+                self.s0, self.s1, cs0 = (sigma0.expand(B, C, H, W).contiguous(),
+                                         sigma1.expand(B, C, H, W).contiguous(), C)
         self.invD0, self.invD1 = invD0.contiguous(), invD1.contiguous()
         self.K = K.reshape(B, 4).contiguous()
         self.m0 = obj_mask0.reshape(B, 1, H, W).to(torch.uint8).contiguous() if obj_mask0 is not None else None
         self.m1 = obj_mask1.reshape(B, 1, H, W).to(torch.uint8).contiguous() if obj_mask1 is not None else None
         flags = N.REMOVE_TRU_SIGMA if remove_tru_sigma else 0
+        if no_uncertainty:
+            flags |= N.NO_UNCERTAINTY
         if combine_icp:
             if depth0 is None or depth1 is None:
                 raise ValueError("combine_icp needs depth0 and depth1")

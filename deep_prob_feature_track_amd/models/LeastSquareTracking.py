@@ -8,11 +8,12 @@ on libdpft_ic.so through `TrustRegionInverseWUncertainty`; the encoder and
 init-pose networks run as PyTorch modules on the same device.
 
 Supported: track_type 'U_IC' (uncertainty_type != 'None', direction 'inverse')
-with encoders RGB / ConvRGBD / ConvRGBD2, identity or learned init pose,
-remove_tru_sigma, uncer_prop (returns JtWJ) and object masks, inference mode.
-The reference's other trackers (IC, U_FC, ICP) and training-mode forward raise
-NotImplementedError -- the reference itself cannot train on torch 2.x
-(algorithms.py:874-875).  Visualisation / logging arguments are accepted and
+and 'IC' (uncertainty_type 'None': TrustRegionBase with M-estimator 'None' and
+solver 'Direct-Nodamping') with encoders RGB / ConvRGBD / ConvRGBD2, identity or
+learned init pose, remove_tru_sigma, combine_ICP, uncer_prop (returns JtWJ) and
+object masks, inference mode.  The reference's U_FC / ICP-only trackers and
+training-mode forward raise NotImplementedError -- the reference itself cannot
+train on torch 2.x (algorithms.py:874-875).  Visualisation / logging arguments are accepted and
 ignored (they only draw with cv2 / tensorboard).
 """
 import types
@@ -21,7 +22,7 @@ import torch
 import torch.nn as nn
 
 from .algorithms import (DeepRobustEstimator, DirectSolverNet, FeaturePyramid, ImagePyramids, PoseNet, ScaleNet,
-                         SFMPoseNet, TrustRegionInverseWUncertainty)
+                         SFMPoseNet, TrustRegionBase, TrustRegionInverseWUncertainty)
 from .submodules import color_normalize
 from .. import ic
 
@@ -116,13 +117,18 @@ class LeastSquareTracking(nn.Module):
         else:
             raise NotImplementedError("Not supported tracking method, check again about the configs of "
                                       "uncertainty and direction.")
-        if self.track_type != 'U_IC':
-            raise NotImplementedError(f"track type {self.track_type}: this build implements the U_IC solver only")
+        if self.track_type not in ('U_IC', 'IC'):
+            raise NotImplementedError(f"track type {self.track_type}: this build implements the U_IC and IC solvers")
         for i in range(4):
-            setattr(self, f'tr_update{i}', TrustRegionInverseWUncertainty(
-                max_iter_per_pyr, mEst_func=mEst_funcs[i], solver_func=solver_funcs[i], timers=timers,
-                combine_icp=self.combine_icp, scale_func=scaler_funcs[i], uncer_prop=options.train_uncer_prop,
-                remove_tru_sigma=remove_tru_sigma))
+            if self.track_type == 'IC':
+                solver = TrustRegionBase(max_iter_per_pyr, mEst_func=mEst_funcs[i], solver_func=solver_funcs[i],
+                                         timers=timers)
+            else:
+                solver = TrustRegionInverseWUncertainty(
+                    max_iter_per_pyr, mEst_func=mEst_funcs[i], solver_func=solver_funcs[i], timers=timers,
+                    combine_icp=self.combine_icp, scale_func=scaler_funcs[i], uncer_prop=options.train_uncer_prop,
+                    remove_tru_sigma=remove_tru_sigma)
+            setattr(self, f'tr_update{i}', solver)
 
         # ---- init-pose network (295-309)
         if self.predict_init_pose:
@@ -141,11 +147,17 @@ class LeastSquareTracking(nn.Module):
         (I0, I1, x0, x1, sigma0, sigma1, dpt0, dpt1, inv_d0, inv_d1, m0, m1, poseI) = self._preprocess(
             img0, img1, depth0, depth1, poseI=None, obj_mask0=obj_mask0, obj_mask1=obj_mask1)
         pose = poseI
-        # the weight prior of level 3 (346) only feeds learned ICP scalers, which are not offered
+        # the weight prior of level 3 (346) only feeds learned ICP scalers / M-estimators, not offered
         for l in (3, 2, 1, 0):
-            out = getattr(self, f'tr_update{l}')(
-                pose, x0[l], x1[l], inv_d0[l], inv_d1[l], K / float(1 << l), sigma0=sigma0[l], sigma1=sigma1[l],
-                wPrior=None, vis_res=False, depth0=dpt0[l], depth1=dpt1[l], obj_mask0=m0[l], obj_mask1=m1[l])
+            tr = getattr(self, f'tr_update{l}')
+            Kl = K / float(1 << l)
+            if self.track_type == 'IC':
+                out = tr(pose, x0[l], x1[l], inv_d0[l], inv_d1[l], Kl, None, vis_res=False,
+                         obj_mask0=m0[l], obj_mask1=m1[l])
+            else:
+                out = tr(pose, x0[l], x1[l], inv_d0[l], inv_d1[l], Kl, sigma0=sigma0[l], sigma1=sigma1[l],
+                         wPrior=None, vis_res=False, depth0=dpt0[l], depth1=dpt1[l], obj_mask0=m0[l],
+                         obj_mask1=m1[l])
             pose = out[0]
         return pose
 
@@ -155,9 +167,13 @@ class LeastSquareTracking(nn.Module):
         (I0, I1, x0, x1, sigma0, sigma1, dpt0, dpt1, inv_d0, inv_d1, m0, m1, poseI) = self._preprocess(
             img0, img1, depth0, depth1, poseI=poseI, obj_mask0=obj_mask0, obj_mask1=obj_mask1)
         i = level_i
-        loss = self.tr_update0.forward_residuals(
-            poseI, x0[i], x1[i], inv_d0[i], inv_d1[i], K / float(1 << i), sigma0=sigma0[i], sigma1=sigma1[i],
-            wPrior=None, vis_res=False, depth0=dpt0[i], depth1=dpt1[i], obj_mask0=m0[i], obj_mask1=m1[i])
+        if self.track_type == 'IC':
+            loss = self.tr_update0.forward_residuals(poseI, x0[i], x1[i], inv_d0[i], inv_d1[i], K / float(1 << i),
+                                                     None, vis_res=False, obj_mask0=m0[i], obj_mask1=m1[i])
+        else:
+            loss = self.tr_update0.forward_residuals(
+                poseI, x0[i], x1[i], inv_d0[i], inv_d1[i], K / float(1 << i), sigma0=sigma0[i], sigma1=sigma1[i],
+                wPrior=None, vis_res=False, depth0=dpt0[i], depth1=dpt1[i], obj_mask0=m0[i], obj_mask1=m1[i])
         return poseI, loss
 
     def prepare(self, img0, img1, depth0, depth1, obj_mask0=None, obj_mask1=None):
@@ -172,7 +188,10 @@ class LeastSquareTracking(nn.Module):
         (I0, I1, x0, x1, sigma0, sigma1, dpt0, dpt1, inv_d0, inv_d1, m0, m1, _) = prepared
         i = level_i
         tr = self.tr_update0
-        kw = tr._common(x0[i], dpt0[i], dpt1[i], m0[i], m1[i])
+        if self.track_type == 'IC':
+            kw = dict(no_uncertainty=True, obj_mask0=m0[i], obj_mask1=m1[i])
+        else:
+            kw = tr._common(x0[i], dpt0[i], dpt1[i], m0[i], m1[i])
         with torch.no_grad():
             return ic.residual_poses(R, t, x0[i], x1[i], inv_d0[i], inv_d1[i], K / float(1 << i),
                                      sigma0[i], sigma1[i], **kw)

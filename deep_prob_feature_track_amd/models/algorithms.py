@@ -316,7 +316,54 @@ class SFMPoseNet(nn.Module):
         return geometry.pose_vec2mat(self.scale_motion * pose.view(B, 6), rotation_mode='euler')
 
 
-# ------------------------------------------------------------------ the HIP-backed solver
+# ------------------------------------------------------------------ the HIP-backed solvers
+class TrustRegionBase(nn.Module):
+    """Inverse-compositional Gauss-Newton WITHOUT uncertainty -- the 'IC' tracker
+    (algorithms.py:23-139), on libdpft_ic.so (flag DPFT_NO_UNCERTAINTY).
+
+    forward -> (pose [R, t], weights): the constant J^T W J of the template
+    (precompute_Jacobian 103-121, identical in every iteration, so the fused kernel
+    simply recomputes it), JtR of the residual at the current pose with occluded
+    residuals 1e-3 (compute_warped_residual 1919-1957), lev_mar_H damping and the
+    inverse update (DirectSolverNet 'Direct-Nodamping', 1604-1642).  As in the
+    reference, only the first residual sees obj_mask0 (the loop re-evaluates with
+    obj_mask1 alone, 77-78).  Supported: mEstimator 'None', solver 'Direct-Nodamping'."""
+
+    def __init__(self, max_iter=3, mEst_func=None, solver_func=None, timers=None):
+        super().__init__()
+        self.max_iterations = max_iter
+        self.mEstimator = mEst_func
+        self.directSolver = solver_func
+        self.timers = timers
+
+    def _check(self, x0):
+        if torch.is_grad_enabled() and x0.requires_grad:
+            raise NotImplementedError("the HIP IC solver is inference-only (no backward kernels)")
+        if self.mEstimator is not None and getattr(self.mEstimator, 'D', -1) > 0:
+            raise NotImplementedError("learned M-estimators are not supported by the fused HIP solver")
+        if self.directSolver is not None and getattr(self.directSolver, 'type', 0) != DirectSolverNet.SOLVER_NO_DAMPING:
+            raise NotImplementedError("only the 'Direct-Nodamping' solver is supported by the fused HIP solver")
+
+    def forward(self, pose, x0, x1, invD0, invD1, K, wPrior=None, vis_res=False, obj_mask0=None, obj_mask1=None):
+        self._check(x0)
+        B, C, H, W = x0.shape
+        with torch.no_grad():
+            for it in range(self.max_iterations):
+                R, t, _, _, _ = ic.iterate(pose, x0, x1, invD0, invD1, K, None, None, first=(it == 0),
+                                           no_uncertainty=True, obj_mask0=obj_mask0 if it == 0 else None,
+                                           obj_mask1=obj_mask1)
+                pose = [R, t]
+        weights = torch.ones((1, 1, 1, 1), dtype=x0.dtype, device=x0.device).expand(B, C, H, W)
+        return pose, weights
+
+    def forward_residuals(self, pose, x0, x1, invD0, invD1, K, wPrior=None, vis_res=False, obj_mask0=None,
+                          obj_mask1=None):
+        self._check(x0)
+        with torch.no_grad():
+            return ic.residual_level(pose, x0, x1, invD0, invD1, K, None, None, no_uncertainty=True,
+                                     obj_mask0=obj_mask0, obj_mask1=obj_mask1)
+
+
 class TrustRegionInverseWUncertainty(nn.Module):
     """Inverse-compositional, uncertainty-weighted Gauss-Newton with Levenberg
     damping (algorithms.py:579-997), one level per call, on libdpft_ic.so.

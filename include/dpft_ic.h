@@ -54,6 +54,9 @@ extern "C" {
 /* flags of DpftLevelDesc */
 #define DPFT_REMOVE_TRU_SIGMA 0x1u /* --remove_tru_sigma (algorithms.py:1975-1980) */
 #define DPFT_COMBINE_ICP      0x2u /* --combine_ICP (algorithms.py:668-689)        */
+#define DPFT_NO_UNCERTAINTY   0x4u /* IC tracker, TrustRegionBase (algorithms.py:23-139):
+                                      sigma = 1, s0/s1 ignored (may be NULL), occluded
+                                      residual 1e-3; excludes the two flags above     */
 
 /* device status word bits */
 #define DPFT_STATUS_NONFINITE 0x1u /* a JtJ / JtR reduction was not finite         */

@@ -45,9 +45,9 @@ def test_state_dict_surface_cases(name):
 
 def test_unsupported_tracker_types_raise():
     spec = G.MODEL_CASES["convrgbd2_c8"]
-    with pytest.raises(NotImplementedError):
-        LeastSquareTracking(spec["encoder"], "None", 3, "None", "Direct-Nodamping",
-                            options=default_options(**spec["opts"]))  # IC tracker
+    m = LeastSquareTracking(spec["encoder"], "None", 3, "None", "Direct-Nodamping",
+                            options=default_options(**spec["opts"]))  # IC tracker: supported
+    assert m.track_type == "IC"
     with pytest.raises(NotImplementedError):
         LeastSquareTracking(spec["encoder"], "laplacian", 3, "None", "Direct-Nodamping", direction="forward",
                             options=default_options(**spec["opts"]))  # U_FC tracker
@@ -101,7 +101,7 @@ def test_forward_and_residual_match_reference(name):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("name", ["convrgbd2_c8", "convrgbd2_c8_icp", "rgb_identity_masks"])
+@pytest.mark.parametrize("name", ["convrgbd2_c8", "convrgbd2_c8_icp", "rgb_identity_masks", "convrgbd_c8_ic_masks"])
 def test_convergence_basin_landscape_matches_reference(name):
     """The multi-pose residual sweep equals the reference's one-compute_residual-per-pose
     loop (convergence_basin.py:340-369, 405-426) at levels 0 and 1."""
