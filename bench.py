@@ -38,6 +38,9 @@ def parse():
     p.add_argument("--kernel-reps", type=int, default=50)
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--no-graph", action="store_true")
+    p.add_argument("--layout", choices=["c4", "nchw"], default="c4",
+                   help="resident feature layout the timed solve reads (c4: channel-quad, the solver's native one)")
+    p.add_argument("--no-compare", action="store_true", help="skip the secondary timing of the other layout")
     return p.parse_args()
 
 
@@ -108,40 +111,64 @@ def main():
     from deep_prob_feature_track_amd import ic, shard
 
     B = a.batch_per_gpu
-    sel, levels, K = make_inputs(B, rank, device)
-    solver = ic.PyramidSolver(levels, K, iters=ITERS, remove_tru_sigma=True)
+    sel, levels_nchw, K = make_inputs(B, rank, device)
+
+    def packed(levels):
+        return [dict(d, x0=ic.pack_features(d["x0"]), x1=ic.pack_features(d["x1"])) for d in levels]
+
+    def pack_time_us(levels, reps=10):
+        """One-time NCHW -> channel-quad conversion of both feature pyramids (not in the step)."""
+        packed(levels)
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        for _ in range(reps):
+            packed(levels)
+        e1.record()
+        torch.cuda.synchronize()
+        return e0.elapsed_time(e1) / reps * 1e3
+
+    levels = packed(levels_nchw) if a.layout == "c4" else levels_nchw
     R_init = torch.eye(3, device=device).repeat(B, 1, 1).contiguous()
     t_init = torch.zeros(B, 3, device=device)
-    R = R_init.clone()
-    t = t_init.clone()
+
+    def make_step(levels):
+        solver = ic.PyramidSolver(levels, K, iters=ITERS, remove_tru_sigma=True)
+        R = R_init.clone()
+        t = t_init.clone()
+
+        def solve():
+            R.copy_(R_init)
+            t.copy_(t_init)
+            solver.run(R, t)
+
+        # eager warm-up (also validates), then capture the whole 4-level solve into one graph
+        solve()
+        torch.cuda.synchronize()
+        ic.check_status(solver.status)
+        graph = None
+        if not a.no_graph:
+            s = torch.cuda.Stream(device)
+            s.wait_stream(torch.cuda.current_stream(device))
+            with torch.cuda.stream(s):
+                solve()
+            torch.cuda.current_stream(device).wait_stream(s)
+            graph = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(graph):
+                solve()
+            torch.cuda.synchronize()
+
+        def run():
+            if graph is not None:
+                graph.replay()
+            else:
+                solve()
+        return solver, R, t, run, graph is not None
+
+    solver, R, t, run, graphed = make_step(levels)
     gathered = torch.empty(world * B, 12, device=device) if world > 1 else None
 
-    def solve():
-        R.copy_(R_init)
-        t.copy_(t_init)
-        solver.run(R, t)
-
-    # eager warm-up (also validates), then capture the whole 4-level solve into one graph
-    solve()
-    torch.cuda.synchronize()
-    ic.check_status(solver.status)
-    graph = None
-    if not a.no_graph:
-        s = torch.cuda.Stream(device)
-        s.wait_stream(torch.cuda.current_stream(device))
-        with torch.cuda.stream(s):
-            solve()
-        torch.cuda.current_stream(device).wait_stream(s)
-        graph = torch.cuda.CUDAGraph()
-        with torch.cuda.graph(graph):
-            solve()
-        torch.cuda.synchronize()
-
     def step():
-        if graph is not None:
-            graph.replay()
-        else:
-            solve()
+        run()
         if world > 1:
             shard.gather_poses(R, t, out=gathered)
 
@@ -189,9 +216,29 @@ def main():
     alg_bytes = solver.algorithmic_bytes(0)
     achieved = alg_bytes / (kern_us * 1e-6) / 1e9
 
+    # secondary (rank 0 only, not the headline): the same solve from the other resident
+    # layout, and the one-time cost of packing NCHW pyramids into the channel-quad layout
+    other = None
+    if rank == 0 and not a.no_compare:
+        other_layout = "nchw" if a.layout == "c4" else "c4"
+        o_solver, o_R, o_t, o_run, _ = make_step(levels_nchw if other_layout == "nchw" else packed(levels_nchw))
+        for _ in range(a.warmup):
+            o_run()
+        torch.cuda.synchronize()
+        tt0 = time.perf_counter()
+        for _ in range(a.steps):
+            o_run()
+        torch.cuda.synchronize()
+        o_el = time.perf_counter() - tt0
+        dpose = max((o_R - R).abs().max().item(), (o_t - t).abs().max().item())
+        other = {"layout": other_layout, "ms_per_step": o_el / a.steps * 1e3,
+                 "value": B * LEVELS * ITERS * a.steps / o_el, "max_abs_pose_diff_vs_headline": dpose,
+                 "pack_us_all_levels_both_frames": pack_time_us(levels_nchw)}
+        del o_solver
+
     cpu = None
     if rank == 0 and world == 1 and not a.no_cpu_baseline:
-        best, dR, dt, epe = cpu_baseline(levels, K, R, t)
+        best, dR, dt, epe = cpu_baseline(levels_nchw, K, R, t)
         cpu = {"value": LEVELS * ITERS / best, "unit": "IC iterations/s",
                "cores": torch.get_num_threads(), "kind": "port",
                "sample": "1 pair, 640x480 C=32, 4 levels x 3 iters, oracle/ic_oracle.py (PyTorch-CPU fp32 "
@@ -209,14 +256,15 @@ def main():
             "config": {"workload": "cfg2/cfg3 shard: 640x480, C=32, Cs=1, 4 levels x 3 GN iters, "
                                    "remove_tru_sigma, B pairs per GPU", "pairs_per_gpu": B,
                        "global_batch": world * B, "parallelism": f"pair-sharded x{world}, RCCL all-gather of poses",
-                       "graph": graph is not None},
+                       "graph": graphed, "feature_layout": a.layout},
             "pairs_per_s": world * B * a.steps / elapsed,
             "l0_iters_per_s": world * B * ITERS * a.steps / elapsed,
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": achieved / HBM_PEAK_GBS, "traffic": None,
-                         "kernel": "ic_reduce_kernel<32,true> (level 0)", "kernel_us": kern_us,
-                         "algorithmic_bytes_per_launch": alg_bytes},
+                         "kernel": f"ic_reduce_kernel<32,Cs=1,tru,U_IC,{a.layout}> (level 0, + in-kernel finalize)",
+                         "kernel_us": kern_us, "algorithmic_bytes_per_launch": alg_bytes},
             "cpu_baseline": cpu,
+            "other_layout": other,
         }
         print(json.dumps(line), flush=True)
     if world > 1:

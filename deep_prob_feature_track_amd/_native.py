@@ -16,6 +16,7 @@ LIB_PATH = os.path.join(_HERE, "libdpft_ic.so")
 REMOVE_TRU_SIGMA = 0x1
 COMBINE_ICP = 0x2
 NO_UNCERTAINTY = 0x4
+FEATURES_C4 = 0x8
 STATUS_NONFINITE = 0x1
 ABI_VERSION = 1
 
@@ -40,7 +41,7 @@ class LevelTensors(ctypes.Structure):
 EXPORTS = ("dpft_workspace_size", "dpft_ic_solve_level", "dpft_ic_iterate", "dpft_ic_residual_level",
            "dpft_residual_poses_workspace_size", "dpft_ic_residual_poses",
            "dpft_ic_reduce_only", "dpft_ic_debug_pixels", "dpft_preprocess_workspace_size",
-           "dpft_preprocess_depth", "dpft_version", "dpft_last_error")
+           "dpft_preprocess_depth", "dpft_pack_features", "dpft_version", "dpft_last_error")
 
 _lib = None
 
@@ -76,6 +77,8 @@ def lib():
     L.dpft_preprocess_depth.argtypes = [vp, ctypes.c_int32, ctypes.c_int32, ctypes.c_int32, ctypes.c_int32,
                                         P(vp), P(vp), vp, sz, vp]
     L.dpft_preprocess_depth.restype = ctypes.c_int
+    L.dpft_pack_features.argtypes = [vp, vp, ctypes.c_int32, ctypes.c_int32, ctypes.c_int32, ctypes.c_int32, vp]
+    L.dpft_pack_features.restype = ctypes.c_int
     L.dpft_version.argtypes = []
     L.dpft_version.restype = ctypes.c_int
     L.dpft_last_error.argtypes = []

@@ -59,6 +59,8 @@ typedef int Rsrc __attribute__((ext_vector_type(4)));
 typedef float f32x2 __attribute__((ext_vector_type(2)));
 __device__ float llvm_buf_load_f32(Rsrc r, int voff, int soff, int aux) __asm("llvm.amdgcn.raw.buffer.load.f32");
 __device__ f32x2 llvm_buf_load_f32x2(Rsrc r, int voff, int soff, int aux) __asm("llvm.amdgcn.raw.buffer.load.v2f32");
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+__device__ f32x4 llvm_buf_load_f32x4(Rsrc r, int voff, int soff, int aux) __asm("llvm.amdgcn.raw.buffer.load.v4f32");
 
 namespace {
 
@@ -67,6 +69,18 @@ constexpr int kTileW = 64;             // one wave = 64 consecutive pixels of a 
 constexpr int kRowsPerStep = 4;        // one row per wave per step
 #ifndef DPFT_RING
 #define DPFT_RING 2
+#endif
+#ifndef DPFT_RPL
+#define DPFT_RPL 1
+#endif
+#ifndef DPFT_ROWMAJOR
+#define DPFT_ROWMAJOR 0
+#endif
+#ifndef DPFT_ABL
+#define DPFT_ABL 0  // ablation builds for profiling only (1: no channel loop, 2: channel loads only)
+#endif
+#ifndef DPFT_RPL4
+#define DPFT_RPL4 1
 #endif
 #ifndef DPFT_CK
 #define DPFT_CK 2
@@ -79,6 +93,8 @@ constexpr int kRowsPerStep = 4;        // one row per wave per step
 #endif
 constexpr int kCK = DPFT_CK;           // channels per pipeline unit
 constexpr int kRing = DPFT_RING;       // load slots in flight ring (kRing - 1 units ahead)
+constexpr int kRPL = DPFT_RPL;         // image rows per lane (Cs == 1 kernels)
+constexpr int kRPL4 = DPFT_RPL4;       // image rows per lane (channel-quad layout)
 constexpr int kLdsW = kTileW + 2;      // 1-pixel halo each side
 constexpr int kLdsH = kRowsPerStep + 2;
 constexpr int kMaxSteps = DPFT_MAX_STEPS;  // up to 4 * kMaxSteps rows per workgroup
@@ -241,6 +257,13 @@ __device__ __forceinline__ float bil4(float a, float b, float c, float d, const 
 __device__ __forceinline__ float bil(const float* __restrict__ p, const Taps& t) {
   return bil4(p[t.o00], p[t.o01], p[t.o10], p[t.o11], t);
 }
+// Channel c of a feature tensor in NCHW (stride 1) or channel-quad layout (stride 4).
+__device__ __forceinline__ const float* chan_base(const float* fb, int c, int HW, bool c4) {
+  return c4 ? fb + (size_t)(c >> 2) * 4 * HW + (c & 3) : fb + (size_t)c * HW;
+}
+__device__ __forceinline__ float bil_s(const float* __restrict__ p, const Taps& t, int s) {
+  return bil4(p[t.o00 * s], p[t.o01 * s], p[t.o10 * s], p[t.o11 * s], t);
+}
 __device__ __forceinline__ float bil_u8(const uint8_t* __restrict__ p, const Taps& t) {
   return bil4((float)p[t.o00], (float)p[t.o01], (float)p[t.o10], (float)p[t.o11], t);
 }
@@ -308,7 +331,7 @@ struct IterParams {
   uint32_t* ctrl;        // see kCtl*
   const uint32_t* ext;   // sigma0 extrema of this level (order-encoded min, max)
   float* rec;
-  int nbpp, per_pair, row_groups;  // reduce kernel schedule (see ic_reduce_kernel)
+  int nbpp, per_pair, row_groups, rps;  // reduce kernel schedule (see ic_reduce_kernel); rps = rows per step
   int fin_on;      // 0: records only (timing hook); 1: last workgroup finalizes
   FinParams fin;
 };
@@ -435,6 +458,7 @@ __device__ __forceinline__ Rsrc rsrc(const void* p, uint32_t bytes) {
 }
 __device__ __forceinline__ float bld(Rsrc r, int voff, int soff) { return llvm_buf_load_f32(r, voff, soff, 0); }
 __device__ __forceinline__ f32x2 bld2(Rsrc r, int voff, int soff) { return llvm_buf_load_f32x2(r, voff, soff, 0); }
+__device__ __forceinline__ f32x4 bld4(Rsrc r, int voff, int soff) { return llvm_buf_load_f32x4(r, voff, soff, 0); }
 
 struct Gather4 {
   float a, b, c, d;  // the two loaded pairs: (row y0: a, b), (row y1: c, d)
@@ -500,9 +524,20 @@ __device__ __forceinline__ void sobel_cols(float top, float mid, float bot, floa
   gy = y * inv;
 }
 
-struct ChanLoads {
-  float t, m, b;  // f0 column in rows y-1, y, y+1
-  Gather4 g;      // f1 taps
+// One channel's loads for a lane holding R vertically adjacent pixels:
+// f0 column rows y0-1 .. y0+R (f[j] = row y0-1+j) and the f1 taps of each pixel.
+template <int R>
+struct ChanLoadsR {
+  float f[R + 2];
+  Gather4 g[R];
+};
+// Channel-quad layout (DPFT_FEATURES_C4): one 16-byte load per row / tap carries
+// 4 channels.  t[r][0..3] = taps (x0, y0), (x0 + 1, y0), (x0, y1), (x0 + 1, y1)
+// of the pair bases (see gather4).
+template <int R>
+struct QuadLoadsR {
+  f32x4 f[R + 2];
+  f32x4 t[R][4];
 };
 
 // ============================================================ ICP term (combine_ICP)
@@ -980,9 +1015,11 @@ __device__ void finalize_loss(const FinParams& q) {
 // MODE: 0 = U_IC (TrustRegionInverseWUncertainty), 1 = U_IC + combine_ICP,
 //       2 = IC without uncertainty (TrustRegionBase, algorithms.py:23-139: sigma = 1,
 //           J = Jf_x Jx + Jf_y Jy (1867-1882), occluded residual 1e-3 (1955)).
-template <int CT, bool CS1, bool TRU, int MODE>
+template <int CT, bool CS1, bool TRU, int MODE, bool C4>
 __global__ __launch_bounds__(kThreads, DPFT_MIN_WAVES) void ic_reduce_kernel(IterParams p) {
   constexpr bool ICP = MODE == 1, NOSIG = MODE == 2;
+  static_assert(!C4 || CS1, "the channel-quad layout needs one sigma plane");
+  constexpr int R = C4 ? kRPL4 : (CS1 ? kRPL : 1);  // rows per lane
   constexpr float kFill = NOSIG ? 1e-3f : 1e-6f;  // weighted residual of invalid pixels
   const int C = CT > 0 ? CT : p.C;
   __shared__ float lds_ext[TRU ? 2 * 7 : 1][kThreads];  // extremum corrections (6 + count), min then max
@@ -990,19 +1027,13 @@ __global__ __launch_bounds__(kThreads, DPFT_MIN_WAVES) void ic_reduce_kernel(Ite
 
   const int tid = threadIdx.x, lane = tid & 63, wave = wave_id();
   const int W = p.W, H = p.H, HW = H * W;
-#ifndef DPFT_REMAP
-#define DPFT_REMAP 1
-#endif
-#ifndef DPFT_ORDER
-#define DPFT_ORDER 1
-#endif
-  const int kb = DPFT_REMAP ? xcd_remap(blockIdx.x, gridDim.x) : blockIdx.x;
+  const int kb = xcd_remap(blockIdx.x, gridDim.x);
   const int b = kb / p.nbpp, jb = kb - b * p.nbpp;
   const int seg_begin = b * p.per_pair + (int)(((long)p.per_pair * jb) / p.nbpp);
   const int seg_end = b * p.per_pair + (int)(((long)p.per_pair * (jb + 1)) / p.nbpp);
   const float g0min = TRU ? dec_ord(p.ext[0]) : 0.f, g0max = TRU ? dec_ord(p.ext[1]) : 0.f;
   const uint32_t planeB = (uint32_t)HW * 4u;
-  const int nch = (C + kCK - 1) / kCK;
+  const int nch = C4 ? C / 4 : (C + kCK - 1) / kCK;    // one unit = one channel quad / kCK channels
   const int nunits = (nch + kRing - 1) / kRing * kRing;  // units per step, padded to the ring (empty tail units)
 
   const float fx = p.K[4 * b + 0], fy = p.K[4 * b + 1], cx = p.K[4 * b + 2], cy = p.K[4 * b + 3];
@@ -1031,164 +1062,131 @@ __global__ __launch_bounds__(kThreads, DPFT_MIN_WAVES) void ic_reduce_kernel(Ite
     for (int k = 0; k < 14; ++k) lds_ext[k][tid] = 0.0f;
   }
 
-  // tile -> (column strip, row of this wave); rows past H are clamped for the
-  // prefetch and skipped by the wave (wave-uniform)
+  // tile -> (column strip, first row of this wave); rows past H are clamped for
+  // the loads and skipped by the accumulation
+  // Tile order.  Channel-quad layout: column-major, a workgroup walks DOWN a
+  // 62-column strip, so the stencil / tap rows shared with the tile above are more
+  // often still in this XCD's L2 (measured L0 fetch 1.05 GB vs 1.13 GB row-major,
+  // 212 vs 217 us).  NCHW: row-major (column-major measured 12 % slower there).
+  constexpr bool kColMajor = C4 && !DPFT_ROWMAJOR;
   auto tile_pos = [&](int i, int& xs, int& y) {
     const int local = i - b * p.per_pair;
-#if DPFT_ORDER == 0
-    const int tx = local / p.row_groups;
-    y = (local - tx * p.row_groups) * kRowsPerStep + wave;
-#else
-    const int ty = local / p.tiles_x;
-    const int tx = local - ty * p.tiles_x;
-    y = ty * kRowsPerStep + wave;
-#endif
+    int tx, ty;
+    if (kColMajor) {
+      tx = local / p.row_groups;
+      ty = local - tx * p.row_groups;
+    } else {
+      ty = local / p.tiles_x;
+      tx = local - ty * p.tiles_x;
+    }
+    y = ty * p.rps + wave * R;
     xs = tx * kTileOut - 1 + lane;                  // this lane's image column (may be -1 or >= W)
   };
-  float d_cur;
-  {
-    int xs0, y0;
-    tile_pos(seg_begin, xs0, y0);
-    d_cur = bld(rd0, min(y0, H - 1) * W * 4 + min(max(xs0, 0), W - 1) * 4, 0);
-  }
-  for (int it = seg_begin; it < seg_end; ++it) {
-    int xs, y;
-    tile_pos(it, xs, y);
-    const int xc = min(max(xs, 0), W - 1);          // clamped: replicate padding of the stencil
-    const bool out_lane = (lane >= 1) && (lane <= kTileOut) && (xs < W);
-    const int colv = xc * 4;
-    const float d = d_cur;
-    if (it + 1 < seg_end) {
-      int xn, yn;
-      tile_pos(it + 1, xn, yn);
-      d_cur = bld(rd0, min(yn, H - 1) * W * 4 + min(max(xn, 0), W - 1) * 4, 0);
+  // ---- per-tile frame: warp, taps, occlusion inputs, masks (geometry.py:291-350, algorithms.py:1999-2008)
+  struct Frame {
+    int y0, xc, colv;
+    bool out_lane, skip;  // skip: wave-uniform, every row of this wave is past the image
+    int rows[R + 2];      // byte offsets of rows y0-1 .. y0+R, replicate-clamped
+    float d[R];
+    Warp wp[R];
+    Taps tp[R];           // only ob0 / ob1 are read after make_frame
+    PairWeights pw[R];
+    Gather4 gd1[R], gs1[R];
+    bool m0[R];
+    float m1[R];
+    float s0r[R + 2];
+  };
+  auto load_d = [&](int it, float (&dv)[R]) {
+    int xs, y0;
+    tile_pos(it, xs, y0);
+#pragma unroll
+    for (int r = 0; r < R; ++r) dv[r] = bld(rd0, min(y0 + r, H - 1) * W * 4 + min(max(xs, 0), W - 1) * 4, 0);
+  };
+  // frame of tile `it` from its inverse depths; issues the frame's gathers (consumed by pixel_terms)
+  auto make_frame = [&](int it, const float (&dv)[R], Frame& F) {
+    int xs;
+    tile_pos(it, xs, F.y0);
+    F.xc = min(max(xs, 0), W - 1);  // clamped: replicate padding of the stencil
+    F.out_lane = (lane >= 1) && (lane <= kTileOut) && (xs < W);
+    F.colv = F.xc * 4;
+    F.skip = __builtin_amdgcn_readfirstlane(F.y0) >= H;
+    if (F.skip) return;
+#pragma unroll
+    for (int j = 0; j < R + 2; ++j) F.rows[j] = min(max(F.y0 - 1 + j, 0), H - 1) * W * 4;
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+      const int yr = min(F.y0 + r, H - 1);
+      F.d[r] = dv[r];
+      F.wp[r] = warp_point(F.xc, yr, dv[r], Rm, tv, fx, fy, cx, cy);
+      F.tp[r] = make_taps(F.wp[r].u, F.wp[r].v, H, W);
+      F.pw[r] = pair_weights(F.tp[r]);
+      F.gd1[r] = gather4(rd1, F.tp[r], 0);
+      F.m0[r] = m0b ? (m0b[yr * W + F.xc] != 0) : true;
+      F.m1[r] = m1b ? bil_u8(m1b, F.tp[r]) : 1.0f;
+      if (CS1 && !NOSIG) F.gs1[r] = gather4(rs1, F.tp[r], 0);
     }
-    if (__builtin_amdgcn_readfirstlane(y) >= H) continue;  // wave-uniform: row past the image
-    const int rT = max(y - 1, 0) * W * 4, rM = y * W * 4, rB = min(y + 1, H - 1) * W * 4;
-    // ---- frame: warp, taps, occlusion, masks (geometry.py:291-350, algorithms.py:1999-2008)
-    const Warp wp = warp_point(xc, y, d, Rm, tv, fx, fy, cx, cy);
-    const Taps tp = make_taps(wp.u, wp.v, H, W);
-    const PairWeights pw = pair_weights(tp);
-    const Gather4 gd1 = gather4(rd1, tp, 0);
-    const bool m0 = m0b ? (m0b[y * W + xc] != 0) : true;
-    const float m1 = m1b ? bil_u8(m1b, tp) : 1.0f;
-    float s0t = 0.f, s0m = 0.f, s0b_ = 0.f;
-    Gather4 gs1;
     if (CS1 && !NOSIG) {
-      s0t = bld(rs0, colv, rT);
-      s0m = bld(rs0, colv, rM);
-      s0b_ = bld(rs0, colv, rB);
-      gs1 = gather4(rs1, tp, 0);
-    }
-
-    ChanLoads S[kRing][kCK];
-    auto issue = [&](ChanLoads (&L)[kCK], int k) {
 #pragma unroll
-      for (int cc = 0; cc < kCK; ++cc) {
-        const int c = k * kCK + cc;
-        if (c < C) {
-          const int po = c * (int)planeB;
-          L[cc].t = bld(rf0, colv, po + rT);
-          L[cc].m = bld(rf0, colv, po + rM);
-          L[cc].b = bld(rf0, colv, po + rB);
-          L[cc].g = gather4(rf1, tp, po);
-        }
+      for (int j = 0; j < R + 2; ++j) F.s0r[j] = bld(rs0, F.colv, F.rows[j]);
+    }
+  };
+
+  // per-pixel occlusion / uncertainty terms of a frame (one sigma plane: before or after the channels)
+  struct PixelTerms {
+    bool invalid[R];
+    float sr0[R], srmin[R], srmax[R], inv_s[R], kk[R], hx[R], hy[R];
+  };
+  auto pixel_terms = [&](const Frame& F, PixelTerms& T) {
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+      const float d1w = bilp(F.gd1[r], F.pw[r]);
+      const bool ok = (F.wp[r].iz > d1w - 0.1f) && (F.wp[r].u > 0.0f) && (F.wp[r].u < (float)W) &&
+                      (F.wp[r].v > 0.0f) && (F.wp[r].v < (float)H);
+      T.invalid[r] = !ok || !F.out_lane || !F.m0[r] || !(F.m1[r] > 0.0f);
+      T.sr0[r] = T.srmin[r] = T.srmax[r] = 0.f;
+      T.inv_s[r] = NOSIG ? 1.0f : 0.f;
+      T.kk[r] = T.hx[r] = T.hy[r] = 0.f;
+      if (CS1 && !NOSIG) {
+        sobel_cols(F.s0r[r], F.s0r[r + 1], F.s0r[r + 2], T.hx[r], T.hy[r]);
+        T.sr0[r] = bilp(F.gs1[r], F.pw[r]);
+        T.srmin[r] = T.srmax[r] = T.sr0[r];
+        const float s0m = F.s0r[r + 1];
+        const float sg = sqrtf(T.sr0[r] * T.sr0[r] + s0m * s0m);
+        T.inv_s[r] = __builtin_amdgcn_rcpf(sg);  // 1 ulp; r * (1/sigma) is a continuous weight
+        T.kk[r] = s0m * (T.inv_s[r] * T.inv_s[r] * T.inv_s[r]);
+        if (TRU) T.invalid[r] = T.invalid[r] || (s0m == g0min) || (s0m == g0max);
       }
-    };
-#pragma unroll
-    for (int r = 0; r + 1 < kRing; ++r) issue(S[r], r);
-
-    bool invalid;
-    {
-      const float d1w = bilp(gd1, pw);
-      const bool ok = (wp.iz > d1w - 0.1f) && (wp.u > 0.0f) && (wp.u < (float)W) && (wp.v > 0.0f) &&
-                      (wp.v < (float)H);
-      invalid = !ok || !out_lane || !m0 || !(m1 > 0.0f);
     }
-    float sr0 = 0.f, srmin = 0.f, srmax = 0.f, inv_s = NOSIG ? 1.0f : 0.f, kk = 0.f, hx = 0.f, hy = 0.f;
-    if (CS1 && !NOSIG) {
-      sobel_cols(s0t, s0m, s0b_, hx, hy);
-      sr0 = bilp(gs1, pw);
-      srmin = srmax = sr0;
-      const float sg = sqrtf(sr0 * sr0 + s0m * s0m);
-      inv_s = __builtin_amdgcn_rcpf(sg);  // 1 ulp; r * (1/sigma) is a continuous weight
-      kk = s0m * (inv_s * inv_s * inv_s);
-      if (TRU) invalid = invalid || (s0m == g0min) || (s0m == g0max);
-    }
-    float Saa = 0.f, Sab = 0.f, Sbb = 0.f, Sa = 0.f, Sb = 0.f, Sar = 0.f, Sbr = 0.f;
+  };
 
-    auto unit = [&](int k, ChanLoads (&cur)[kCK], ChanLoads (&nxt)[kCK]) {
-      if (k + kRing - 1 < nunits) issue(nxt, k + kRing - 1);
+  // the seven per-pixel channel sums -> JtJ / JtR / invalid count / extremum corrections
+  struct Sums {
+    float Saa[R], Sab[R], Sbb[R], Sa[R], Sb[R], Sar[R], Sbr[R];
+  };
+  auto finish_pixels = [&](const Frame& F, const PixelTerms& T, Sums& S) {
 #pragma unroll
-      for (int cc = 0; cc < kCK; ++cc) {
-        const int c = k * kCK + cc;
-        if (c >= C) break;
-        float gx, gy;
-        sobel_cols(cur[cc].t, cur[cc].m, cur[cc].b, gx, gy);
-        const float f0v = cur[cc].m;
-        float is_c = inv_s, kk_c = kk, hx_c = hx, hy_c = hy;
-        if (!CS1 && !NOSIG) {
-          const int po = c * (int)planeB;
-          const float st_ = bld(rs0, colv, po + rT), sm_ = bld(rs0, colv, po + rM), sb_ = bld(rs0, colv, po + rB);
-          sobel_cols(st_, sm_, sb_, hx_c, hy_c);
-          const float src = bil(p.s1 + ((size_t)b * p.Cs + c) * HW, tp);
-          const float sg = sqrtf(src * src + sm_ * sm_);
-          is_c = 1.0f / sg;
-          kk_c = sm_ * (is_c * is_c * is_c);
-          if (c == 0) {
-            sr0 = src;
-            srmin = srmax = src;
-            if (TRU) invalid = invalid || (sm_ == g0min) || (sm_ == g0max);
-          } else {
-            srmin = fminf(srmin, src);
-            srmax = fmaxf(srmax, src);
-          }
-        }
-        const float frv = bilp(cur[cc].g, pw);
-        const float r = frv - f0v;
-        const float rw = r * is_c;
-        const float rk = r * kk_c;
-        // na = -a, nb = -b (a, b of algorithms.py:872); the linear sums are negated after the loop
-        const float na = gx * is_c + rk * hx_c;
-        const float nb = gy * is_c + rk * hy_c;
-        Saa += na * na;
-        Sab += na * nb;
-        Sbb += nb * nb;
-        Sa += na;
-        Sb += nb;
-        Sar += na * rw;
-        Sbr += nb * rw;
-      }
-    };
-
-#pragma unroll 1
-    for (int kb = 0; kb < nunits; kb += kRing) {
-#pragma unroll
-      for (int r = 0; r < kRing; ++r) unit(kb + r, S[r], S[(r + kRing - 1) % kRing]);
-    }
-    Sa = -Sa;
-    Sb = -Sb;
-    Sar = -Sar;
-    Sbr = -Sbr;
-
-    if (out_lane) {
+    for (int r = 0; r < R; ++r) {
+      if (!F.out_lane || F.y0 + r >= H) continue;
+      const float Sa = -S.Sa[r], Sb = -S.Sb[r], Sar = -S.Sar[r], Sbr = -S.Sbr[r];
+      const float Saa = S.Saa[r], Sab = S.Sab[r], Sbb = S.Sbb[r];
+      const bool invalid = T.invalid[r];
       float Jx[6], Jy[6];
-      warp_jac(wp.xr, wp.yr, d, fx, fy, Jx, Jy);
+      warp_jac(F.wp[r].xr, F.wp[r].yr, F.d[r], fx, fy, Jx, Jy);
       // weighted residual of invalid pixels is 1e-6 on every channel (algorithms.py:1982-1983)
       const float cA = invalid ? kFill * Sa : Sar;
       const float cB = invalid ? kFill * Sb : Sbr;
-      float P[6], Q[6];
+      float P[6], Qv[6];
 #pragma unroll
       for (int i = 0; i < 6; ++i) {
         P[i] = Saa * Jx[i] + Sab * Jy[i];
-        Q[i] = Sab * Jx[i] + Sbb * Jy[i];
+        Qv[i] = Sab * Jx[i] + Sbb * Jy[i];
       }
       int kq = 0;
 #pragma unroll
       for (int i = 0; i < 6; ++i) {
 #pragma unroll
         for (int j = i; j < 6; ++j) {
-          acc[kq] += P[i] * Jx[j] + Q[i] * Jy[j];
+          acc[kq] += P[i] * Jx[j] + Qv[i] * Jy[j];
           ++kq;
         }
       }
@@ -1196,9 +1194,11 @@ __global__ __launch_bounds__(kThreads, DPFT_MIN_WAVES) void ic_reduce_kernel(Ite
       for (int i = 0; i < 6; ++i) acc[21 + i] -= cA * Jx[i] + cB * Jy[i];
       ninv += invalid ? 1.0f : 0.0f;
       if (ICP) {  // JtWJ += (wJ)^T (wJ), JtR += (wJ)^T (w r)  (algorithms.py:668-689)
-        const float d0v = p.depth0[(size_t)b * HW + y * W + xc];
-        const IcpTerm ic = icp_pixel(wp.xr, wp.yr, d0v, Rm, tv, fx, fy, cx, cy, H, W, p.depth1 + (size_t)b * HW,
-                                     p.nrm1 + (size_t)b * 3 * HW, HW, !m0, m1b, p.icp_w);
+        const int yr = F.y0 + r;
+        const float d0v = p.depth0[(size_t)b * HW + yr * W + F.xc];
+        const IcpTerm ic = icp_pixel(F.wp[r].xr, F.wp[r].yr, d0v, Rm, tv, fx, fy, cx, cy, H, W,
+                                     p.depth1 + (size_t)b * HW, p.nrm1 + (size_t)b * 3 * HW, HW, !F.m0[r], m1b,
+                                     p.icp_w);
         int kq2 = 0;
 #pragma unroll
         for (int i = 0; i < 6; ++i) {
@@ -1210,8 +1210,9 @@ __global__ __launch_bounds__(kThreads, DPFT_MIN_WAVES) void ic_reduce_kernel(Ite
       }
 
       if (TRU) {
-        mn_all = fminf(mn_all, srmin);
-        mx_all = fmaxf(mx_all, srmax);
+        mn_all = fminf(mn_all, T.srmin[r]);
+        mx_all = fmaxf(mx_all, T.srmax[r]);
+        const float sr0 = T.sr0[r];
         const bool le = sr0 <= mn0, ge = sr0 >= mx0;
         if (le || ge) {
           float corr[7];
@@ -1234,6 +1235,216 @@ __global__ __launch_bounds__(kThreads, DPFT_MIN_WAVES) void ic_reduce_kernel(Ite
           }
         }
       }
+    }
+  };
+
+  if constexpr (C4) {
+    // ---- channel-quad layout: the per-pixel weights factor out of the channel sums
+    // (alpha = 1/sigma, bx = kk hx, by = kk hy give na = alpha gx + bx r,
+    // nb = alpha gy + by r, rw = alpha r for every channel), so the channel loop needs
+    // only the taps: nine weight-free sums per pixel,
+    // Q = [gx gx, gx gy, gy gy, gx r, gy r, r r, gx, gy, r], accumulated per channel
+    // pair in packed fp32 (even / odd channels in the two halves).
+    // Quad plane q of pair b = [H][W][4] floats at b * C * HW + q * 4 * HW.
+    // (Issuing the next tile's first quads during this tile -- software pipelining
+    // across tiles -- needs two live frames: 300 VGPRs, one wave per SIMD, 30 % slower.)
+    QuadLoadsR<R> S4[kRing];
+    auto issue4 = [&](const Frame& F, QuadLoadsR<R>& L, int k) {
+      const int po = k * 4 * (int)planeB;
+#pragma unroll
+      for (int j = 0; j < R + 2; ++j) L.f[j] = bld4(rf0, F.colv * 4, po + F.rows[j] * 4);
+#pragma unroll
+      for (int r = 0; r < R; ++r) {
+        L.t[r][0] = bld4(rf1, F.tp[r].ob0 * 16, po);
+        L.t[r][1] = bld4(rf1, F.tp[r].ob0 * 16 + 16, po);
+        L.t[r][2] = bld4(rf1, F.tp[r].ob1 * 16, po);
+        L.t[r][3] = bld4(rf1, F.tp[r].ob1 * 16 + 16, po);
+      }
+    };
+    float d_cur[R];
+    load_d(seg_begin, d_cur);
+    for (int it = seg_begin; it < seg_end; ++it) {
+      float dv[R];
+#pragma unroll
+      for (int r = 0; r < R; ++r) dv[r] = d_cur[r];
+      if (it + 1 < seg_end) load_d(it + 1, d_cur);
+      Frame F;
+      make_frame(it, dv, F);
+      if (F.skip) continue;
+#pragma unroll
+      for (int q = 0; q + 1 < kRing; ++q)
+        if (q < nch) issue4(F, S4[q], q);
+      // resolve the frame's gathers now (issued before the quads: no wait on those), so
+      // that only the taps, weights and epilogue inputs stay live across the channel loop
+      PixelTerms T;
+      pixel_terms(F, T);
+      {
+        f32x2 Q[R][9];
+#pragma unroll
+        for (int r = 0; r < R; ++r)
+#pragma unroll
+          for (int k = 0; k < 9; ++k) Q[r][k] = f32x2{0.f, 0.f};
+        // two channels of row r (lane-neighbour terms by DPP per half)
+        auto chan2 = [&](int r, f32x2 ft, f32x2 fm, f32x2 fb, f32x2 t0, f32x2 t1, f32x2 t2, f32x2 t3) {
+#if DPFT_ABL == 2
+          Q[r][0] += ft + fm + fb + t0 + t1 + t2 + t3;
+          return;
+#endif
+          const f32x2 V = ft + 2.0f * fm + fb;
+          const f32x2 D = fb - ft;
+          const f32x2 x = f32x2{lane_from_right(V.x) - lane_from_left(V.x), lane_from_right(V.y) - lane_from_left(V.y)};
+          const f32x2 y =
+              f32x2{lane_from_left(D.x) + lane_from_right(D.x), lane_from_left(D.y) + lane_from_right(D.y)} + 2.0f * D;
+          const f32x2 n2 = x * x + y * y + 1e-8f;
+          const f32x2 inv = f32x2{__builtin_amdgcn_rsqf(n2.x), __builtin_amdgcn_rsqf(n2.y)};
+          const f32x2 gx = x * inv, gy = y * inv;
+          const PairWeights& w = F.pw[r];
+          const f32x2 res = (t0 * w.w0 + t1 * w.w1 + t2 * w.w2 + t3 * w.w3) - fm;
+          Q[r][0] += gx * gx;
+          Q[r][1] += gx * gy;
+          Q[r][2] += gy * gy;
+          Q[r][3] += gx * res;
+          Q[r][4] += gy * res;
+          Q[r][5] += res * res;
+          Q[r][6] += gx;
+          Q[r][7] += gy;
+          Q[r][8] += res;
+        };
+        auto unit = [&](int k, QuadLoadsR<R>& cur, QuadLoadsR<R>& nxt, bool refill) {
+#if DPFT_ABL == 1
+          return;
+#endif
+          if (refill && k + kRing - 1 < nch) issue4(F, nxt, k + kRing - 1);
+          if (k >= nch) return;
+#pragma unroll
+          for (int h = 0; h < 2; ++h) {  // channels 4k + 2h, 4k + 2h + 1
+#pragma unroll
+            for (int r = 0; r < R; ++r) {
+              auto half = [&](const f32x4& v) { return h ? f32x2{v.z, v.w} : f32x2{v.x, v.y}; };
+              chan2(r, half(cur.f[r]), half(cur.f[r + 1]), half(cur.f[r + 2]), half(cur.t[r][0]),
+                    half(cur.t[r][1]), half(cur.t[r][2]), half(cur.t[r][3]));
+            }
+          }
+        };
+        // every group but the last refills the ring unconditionally (no register merges in the loop)
+#pragma unroll 1
+        for (int kq = 0; kq < nunits - kRing; kq += kRing) {
+#pragma unroll
+          for (int q = 0; q < kRing; ++q) unit(kq + q, S4[q], S4[(q + kRing - 1) % kRing], true);
+        }
+#pragma unroll
+        for (int q = 0; q < kRing; ++q) unit(nunits - kRing + q, S4[q], S4[(q + kRing - 1) % kRing], q == 0);
+
+        Sums S;
+#pragma unroll
+        for (int r = 0; r < R; ++r) {
+          float q[9];
+#pragma unroll
+          for (int k = 0; k < 9; ++k) q[k] = Q[r][k].x + Q[r][k].y;
+          const float A = T.inv_s[r], bx = T.kk[r] * T.hx[r], by = T.kk[r] * T.hy[r], A2 = A * A;
+          S.Saa[r] = A2 * q[0] + 2.0f * A * bx * q[3] + bx * bx * q[5];
+          S.Sab[r] = A2 * q[1] + A * by * q[3] + A * bx * q[4] + bx * by * q[5];
+          S.Sbb[r] = A2 * q[2] + 2.0f * A * by * q[4] + by * by * q[5];
+          S.Sa[r] = A * q[6] + bx * q[8];
+          S.Sb[r] = A * q[7] + by * q[8];
+          S.Sar[r] = A2 * q[3] + A * bx * q[5];
+          S.Sbr[r] = A2 * q[4] + A * by * q[5];
+        }
+        finish_pixels(F, T, S);
+      }
+    }
+  } else {
+    // ---- NCHW layout: per channel, three f0 rows and two tap pairs per pixel
+    float d_cur[R];
+    load_d(seg_begin, d_cur);
+    for (int it = seg_begin; it < seg_end; ++it) {
+      float dv[R];
+#pragma unroll
+      for (int r = 0; r < R; ++r) dv[r] = d_cur[r];
+      if (it + 1 < seg_end) load_d(it + 1, d_cur);
+      Frame F;
+      make_frame(it, dv, F);
+      if (F.skip) continue;
+      const int colv = F.colv;
+      ChanLoadsR<R> S[kRing][kCK];
+      auto issue = [&](ChanLoadsR<R> (&L)[kCK], int k) {
+#pragma unroll
+        for (int cc = 0; cc < kCK; ++cc) {
+          const int c = k * kCK + cc;
+          if (c < C) {
+            const int po = c * (int)planeB;
+#pragma unroll
+            for (int j = 0; j < R + 2; ++j) L[cc].f[j] = bld(rf0, colv, po + F.rows[j]);
+#pragma unroll
+            for (int r = 0; r < R; ++r) L[cc].g[r] = gather4(rf1, F.tp[r], po);
+          }
+        }
+      };
+#pragma unroll
+      for (int q = 0; q + 1 < kRing; ++q) issue(S[q], q);
+      PixelTerms T;
+      pixel_terms(F, T);
+      Sums Sm;
+#pragma unroll
+      for (int r = 0; r < R; ++r) Sm.Saa[r] = Sm.Sab[r] = Sm.Sbb[r] = Sm.Sa[r] = Sm.Sb[r] = Sm.Sar[r] = Sm.Sbr[r] = 0.f;
+
+      // one channel of row r: ft, fm, fb = f0 column above / at / below the pixel, g = f1 taps
+      auto chan = [&](int r, int c, float ft, float fm, float fb, const Gather4& g) {
+        float gx, gy;
+        sobel_cols(ft, fm, fb, gx, gy);
+        float is_c = T.inv_s[r], kk_c = T.kk[r], hx_c = T.hx[r], hy_c = T.hy[r];
+        if (!CS1 && !NOSIG) {  // per-channel sigma (R == 1 here)
+          const int po = c * (int)planeB;
+          const float st_ = bld(rs0, colv, po + F.rows[0]), sm_ = bld(rs0, colv, po + F.rows[1]),
+                      sb_ = bld(rs0, colv, po + F.rows[2]);
+          sobel_cols(st_, sm_, sb_, hx_c, hy_c);
+          const float src = bil(p.s1 + ((size_t)b * p.Cs + c) * HW, F.tp[r]);
+          const float sg = sqrtf(src * src + sm_ * sm_);
+          is_c = 1.0f / sg;
+          kk_c = sm_ * (is_c * is_c * is_c);
+          if (c == 0) {
+            T.sr0[r] = src;
+            T.srmin[r] = T.srmax[r] = src;
+            if (TRU) T.invalid[r] = T.invalid[r] || (sm_ == g0min) || (sm_ == g0max);
+          } else {
+            T.srmin[r] = fminf(T.srmin[r], src);
+            T.srmax[r] = fmaxf(T.srmax[r], src);
+          }
+        }
+        const float frv = bilp(g, F.pw[r]);
+        const float res = frv - fm;
+        const float rw = res * is_c;
+        const float rk = res * kk_c;
+        // na = -a, nb = -b (a, b of algorithms.py:872); the linear sums are negated in finish_pixels
+        const float na = gx * is_c + rk * hx_c;
+        const float nb = gy * is_c + rk * hy_c;
+        Sm.Saa[r] += na * na;
+        Sm.Sab[r] += na * nb;
+        Sm.Sbb[r] += nb * nb;
+        Sm.Sa[r] += na;
+        Sm.Sb[r] += nb;
+        Sm.Sar[r] += na * rw;
+        Sm.Sbr[r] += nb * rw;
+      };
+      auto unit = [&](int k, ChanLoadsR<R> (&cur)[kCK], ChanLoadsR<R> (&nxt)[kCK], bool refill) {
+        if (refill) issue(nxt, k + kRing - 1);
+#pragma unroll
+        for (int cc = 0; cc < kCK; ++cc) {
+          const int c = k * kCK + cc;
+          if (c >= C) break;
+#pragma unroll
+          for (int r = 0; r < R; ++r) chan(r, c, cur[cc].f[r], cur[cc].f[r + 1], cur[cc].f[r + 2], cur[cc].g[r]);
+        }
+      };
+      // every group but the last refills the ring unconditionally (no register merges in the loop)
+#pragma unroll 1
+      for (int kq = 0; kq < nunits - kRing; kq += kRing) {
+#pragma unroll
+        for (int q = 0; q < kRing; ++q) unit(kq + q, S[q], S[(q + kRing - 1) % kRing], true);
+      }
+#pragma unroll
+      for (int q = 0; q < kRing; ++q) unit(nunits - kRing + q, S[q], S[(q + kRing - 1) % kRing], q == 0);
+      finish_pixels(F, T, Sm);
     }
   }
 
@@ -1330,6 +1541,8 @@ __global__ __launch_bounds__(kThreads) void ic_residual_kernel(IterParams p) {
   const int b = rest / p.tiles_y;
   const int W = p.W, H = p.H, HW = H * W, C = p.C;
   const bool tru = (p.flags & DPFT_REMOVE_TRU_SIGMA) != 0;
+  const bool c4 = (p.flags & DPFT_FEATURES_C4) != 0;
+  const int fs = c4 ? 4 : 1;  // element stride of a feature channel
   const float fx = p.K[4 * b + 0], fy = p.K[4 * b + 1], cx = p.K[4 * b + 2], cy = p.K[4 * b + 3];
   float Rm[9], tv[3];
   for (int k = 0; k < 9; ++k) Rm[k] = p.R[9 * ((size_t)pi * p.B + b) + k];
@@ -1352,7 +1565,7 @@ __global__ __launch_bounds__(kThreads) void ic_residual_kernel(IterParams p) {
     float srr = 0.f, smin = INFINITY, smax = -INFINITY, sr0 = 0.f, s00 = 0.f;
     for (int c = 0; c < C; ++c) {
       if (NOSIG) {  // TrustRegionBase.forward_residuals: r = f1(warp) - f0 (algorithms.py:1919-1957)
-        const float r = bil(f1b + (size_t)c * HW, px.tp) - f0b[(size_t)c * HW + pix];
+        const float r = bil_s(chan_base(f1b, c, HW, c4), px.tp, fs) - chan_base(f0b, c, HW, c4)[(size_t)pix * fs];
         srr += r * r;
         continue;
       }
@@ -1365,7 +1578,7 @@ __global__ __launch_bounds__(kThreads) void ic_residual_kernel(IterParams p) {
       }
       smin = fminf(smin, src);
       smax = fmaxf(smax, src);
-      const float r = bil(f1b + (size_t)c * HW, px.tp) - f0b[(size_t)c * HW + pix];
+      const float r = bil_s(chan_base(f1b, c, HW, c4), px.tp, fs) - chan_base(f0b, c, HW, c4)[(size_t)pix * fs];
       const float rw = r / sqrtf(src * src + s0c * s0c);
       srr += rw * rw;
     }
@@ -1456,6 +1669,17 @@ __global__ __launch_bounds__(kThreads) void ic_debug_pixels_kernel(IterParams p,
   o[2 * HW] = bil(p.s1 + (size_t)b * p.Cs * HW, px.tp);
   o[3 * HW] = p.s0[(size_t)b * p.Cs * HW + pix];
   o[4 * HW] = px.invalid ? 1.0f : 0.0f;
+}
+
+// NCHW -> channel-quad layout: thread i = (b, q, pixel) gathers channels 4q..4q+3
+// (four coalesced plane reads) into one 16-byte store.
+__global__ __launch_bounds__(kThreads) void pack_c4_kernel(const float* __restrict__ src, f32x4* __restrict__ dst,
+                                                           long n, int HW) {
+  const long i = (long)blockIdx.x * kThreads + threadIdx.x;
+  if (i >= n) return;
+  const long bq = i / HW, pix = i - bq * HW;  // bq = b * C/4 + q: planes 4 bq .. 4 bq + 3
+  const float* s = src + bq * 4 * HW + pix;
+  dst[i] = f32x4{s[0], s[HW], s[2 * (long)HW], s[3 * (long)HW]};
 }
 
 // sigma0 batch-global min / max (algorithms.py:1976-1977).  Per-workgroup
@@ -1623,6 +1847,8 @@ int check_desc(const DpftLevelDesc* d) {
     return fail(DPFT_E_INVALID, "icp_weight is NaN");
   if ((d->flags & DPFT_NO_UNCERTAINTY) && (d->flags & (DPFT_REMOVE_TRU_SIGMA | DPFT_COMBINE_ICP)))
     return fail(DPFT_E_INVALID, "NO_UNCERTAINTY (IC tracker) excludes REMOVE_TRU_SIGMA and COMBINE_ICP");
+  if ((d->flags & DPFT_FEATURES_C4) && (d->C % 4 != 0 || (d->Cs != 1 && !(d->flags & DPFT_NO_UNCERTAINTY))))
+    return fail(DPFT_E_INVALID, "FEATURES_C4 needs C %% 4 == 0 and one sigma plane (C=%d, Cs=%d)", d->C, d->Cs);
   return DPFT_OK;
 }
 
@@ -1696,7 +1922,9 @@ IterParams make_params(const DpftLevelDesc& d, const DpftLevelTensors& tt, const
   p.ctrl = reinterpret_cast<uint32_t*>(ws);
   p.ext = p.ctrl + kCtlMin;
   p.rec = reinterpret_cast<float*>(static_cast<char*>(ws) + rec_offset(d));
-  p.row_groups = (d.H + kRowsPerStep - 1) / kRowsPerStep;
+  // rows per step of the reduce kernel (4 waves x rows per lane of the instantiation launched)
+  p.rps = 4 * ((d.flags & DPFT_FEATURES_C4) ? kRPL4 : (d.Cs == 1 || (d.flags & DPFT_NO_UNCERTAINTY)) ? kRPL : 1);
+  p.row_groups = (d.H + p.rps - 1) / p.rps;
   p.per_pair = g.tiles_x * p.row_groups;
   p.nbpp = 0;  // set at launch from the kernel's resident capacity
   p.fin_on = 0;
@@ -1767,14 +1995,14 @@ int resident_blocks(const void* kernel) {
   return n;
 }
 
-template <int CT, bool CS1, bool TRU, int MODE>
+template <int CT, bool CS1, bool TRU, int MODE, bool C4 = false>
 int launch_reduce_k(IterParams p, hipStream_t st) {
-  const void* k = reinterpret_cast<const void*>(&ic_reduce_kernel<CT, CS1, TRU, MODE>);
+  const void* k = reinterpret_cast<const void*>(&ic_reduce_kernel<CT, CS1, TRU, MODE, C4>);
   const int cap = resident_blocks(k);
   if (cap <= 0) return fail(DPFT_E_HIP, "occupancy query failed");
   p.nbpp = std::max(1, std::min(cap / p.B, p.per_pair));
   p.fin.nbpp = p.nbpp;
-  hipLaunchKernelGGL((ic_reduce_kernel<CT, CS1, TRU, MODE>), dim3(p.B * p.nbpp), dim3(kThreads), 0, st, p);
+  hipLaunchKernelGGL((ic_reduce_kernel<CT, CS1, TRU, MODE, C4>), dim3(p.B * p.nbpp), dim3(kThreads), 0, st, p);
   return DPFT_OK;
 }
 
@@ -1794,9 +2022,20 @@ int launch_reduce_t(const IterParams& p, hipStream_t st) {
   return tru ? launch_reduce_k<CT, CS1, true, 0>(p, st) : launch_reduce_k<CT, CS1, false, 0>(p, st);
 }
 
+template <int CT>
+int launch_reduce_c4(const IterParams& p, hipStream_t st) {
+  const bool tru = (p.flags & DPFT_REMOVE_TRU_SIGMA) != 0;
+  if (p.flags & DPFT_NO_UNCERTAINTY) return launch_reduce_k<CT, true, false, 2, true>(p, st);
+  if (p.flags & DPFT_COMBINE_ICP)
+    return tru ? launch_reduce_k<CT, true, true, 1, true>(p, st) : launch_reduce_k<CT, true, false, 1, true>(p, st);
+  return tru ? launch_reduce_k<CT, true, true, 0, true>(p, st) : launch_reduce_k<CT, true, false, 0, true>(p, st);
+}
+
 int launch_reduce(const IterParams& p, hipStream_t st) {
   int rc;
-  if (p.Cs == 1) {
+  if (p.flags & DPFT_FEATURES_C4) {
+    rc = p.C == 32 ? launch_reduce_c4<32>(p, st) : launch_reduce_c4<0>(p, st);
+  } else if (p.Cs == 1 || (p.flags & DPFT_NO_UNCERTAINTY)) {
     switch (p.C) {
       case 8: rc = launch_reduce_t<8, true>(p, st); break;
       case 16: rc = launch_reduce_t<16, true>(p, st); break;
@@ -1960,6 +2199,16 @@ int dpft_preprocess_depth(const float* depth, int32_t B, int32_t H, int32_t W, i
   hipLaunchKernelGGL(invd_pyramid_kernel, dim3((unsigned)((n + kThreads - 1) / kThreads), levels), dim3(kThreads), 0,
                      st, depth, B, H, W, ctrl, out);
   return hip_check("invd_pyramid_kernel");
+}
+
+int dpft_pack_features(const float* src, float* dst, int32_t B, int32_t C, int32_t H, int32_t W, void* hip_stream) {
+  if (!src || !dst || src == dst) return fail(DPFT_E_INVALID, "null or aliased pointer");
+  if (B < 1 || C < 4 || C % 4 != 0 || H < 1 || W < 1 || (long)H * W >= (1L << 30))
+    return fail(DPFT_E_INVALID, "bad shape B=%d C=%d H=%d W=%d (C %% 4 == 0 needed)", B, C, H, W);
+  const long n = (long)B * (C / 4) * H * W;
+  hipLaunchKernelGGL(pack_c4_kernel, dim3((unsigned)((n + kThreads - 1) / kThreads)), dim3(kThreads), 0,
+                     static_cast<hipStream_t>(hip_stream), src, reinterpret_cast<f32x4*>(dst), n, H * W);
+  return hip_check("pack_c4_kernel");
 }
 
 int dpft_version(void) { return DPFT_ABI_VERSION; }

@@ -52,12 +52,59 @@ def _sigma_planes(sigma, B, C, H, W):
     return sigma.contiguous(), C
 
 
+def pack_features(x):
+    """Feature map [B,C,H,W] -> channel-quad layout [B,C/4,H,W,4] (dpft_pack_features).
+
+    The packed tensor holds the same values; the solver reads 4 channels of a pixel /
+    bilinear tap with one coalesced 16-byte load (DPFT_FEATURES_C4).  Every solver
+    entry point accepts either form for x0 / x1."""
+    if not x.is_cuda:
+        raise RuntimeError("pack_features needs a device tensor; there is no CPU fallback")
+    if x.dtype != torch.float32 or x.dim() != 4 or x.shape[1] % 4 != 0:
+        raise ValueError(f"need fp32 [B,C,H,W] with C % 4 == 0, got {x.dtype} {tuple(x.shape)}")
+    x = x.contiguous()
+    B, C, H, W = x.shape
+    out = torch.empty(B, C // 4, H, W, 4, dtype=torch.float32, device=x.device)
+    rc = N.lib().dpft_pack_features(_ptr(x), _ptr(out), B, C, H, W, _stream(x.device))
+    N.check(rc, "dpft_pack_features")
+    return out
+
+
+def unpack_features(xp):
+    """Inverse of pack_features (a torch view + copy; tests / inspection only)."""
+    B, Q, H, W, _ = xp.shape
+    return xp.permute(0, 1, 4, 2, 3).reshape(B, 4 * Q, H, W).contiguous()
+
+
+def packable(x, sigma=None, no_uncertainty=False):
+    """True when `x` [B,C,H,W] may run in the channel-quad layout: C % 4 == 0 and
+    one sigma plane (a [B,1,H,W] map or its channel broadcast) or no uncertainty."""
+    if x.dim() != 4 or x.shape[1] % 4 != 0 or not x.is_cuda:
+        return False
+    if no_uncertainty:
+        return True
+    return sigma is not None and sigma.dim() == 4 and (sigma.shape[1] == 1 or sigma.stride(1) == 0)
+
+
+def feature_shape(x):
+    """(B, C, H, W) of a feature map in either layout."""
+    if x.dim() == 5:
+        B, Q, H, W, four = x.shape
+        if four != 4:
+            raise ValueError(f"packed features must be [B,C/4,H,W,4], got {tuple(x.shape)}")
+        return B, 4 * Q, H, W
+    return tuple(x.shape)
+
+
 class LevelCall:
-    """Validated, pointer-ready arguments of one pyramid level."""
+    """Validated, pointer-ready arguments of one pyramid level.
+
+    x0 / x1 are [B,C,H,W] (NCHW) or channel-quad packed [B,C/4,H,W,4]; with
+    pack=True eligible NCHW inputs are packed here (once for all iterations)."""
 
     def __init__(self, x0, x1, invD0, invD1, K, sigma0, sigma1, iters=3, remove_tru_sigma=False,
                  obj_mask0=None, obj_mask1=None, depth0=None, depth1=None, combine_icp=False,
-                 icp_weight=0.01, status=None, no_uncertainty=False):
+                 icp_weight=0.01, status=None, no_uncertainty=False, pack=False):
         if not x0.is_cuda:
             raise RuntimeError("the HIP solver needs device tensors (got CPU); there is no CPU fallback")
         for name, t in (("x0", x0), ("x1", x1), ("invD0", invD0), ("invD1", invD1), ("K", K)):
@@ -65,9 +112,12 @@ class LevelCall:
                 raise TypeError(f"{name} must be float32 (got {t.dtype})")
             if t.device != x0.device:
                 raise ValueError(f"{name} is on {t.device}, expected {x0.device}")
-        B, C, H, W = x0.shape
         if x1.shape != x0.shape:
             raise ValueError(f"x1 {tuple(x1.shape)} != x0 {tuple(x0.shape)}")
+        if pack and packable(x0, sigma0, no_uncertainty):
+            x0, x1 = pack_features(x0), pack_features(x1)
+        c4 = x0.dim() == 5
+        B, C, H, W = feature_shape(x0)
         for name, t in (("invD0", invD0), ("invD1", invD1)):
             if tuple(t.shape) != (B, 1, H, W):
                 raise ValueError(f"{name} shape {tuple(t.shape)} != {(B, 1, H, W)}")
@@ -87,6 +137,10 @@ class LevelCall:
         self.m0 = obj_mask0.reshape(B, 1, H, W).to(torch.uint8).contiguous() if obj_mask0 is not None else None
         self.m1 = obj_mask1.reshape(B, 1, H, W).to(torch.uint8).contiguous() if obj_mask1 is not None else None
         flags = N.REMOVE_TRU_SIGMA if remove_tru_sigma else 0
+        if c4:
+            if cs0 != 1 and not no_uncertainty:
+                raise ValueError("packed features need a single sigma plane ([B,1,H,W] or its broadcast)")
+            flags |= N.FEATURES_C4
         if no_uncertainty:
             flags |= N.NO_UNCERTAINTY
         if combine_icp:
@@ -121,7 +175,8 @@ def check_status(status):
 
 
 def solve_level(pose, x0, x1, invD0, invD1, K, sigma0, sigma1, iters=3, return_jtj=False, check=True, **kw):
-    """`iters` Gauss-Newton steps at one level; returns (R [B,3,3], t [B,3,1][, JtJ [B,6,6]])."""
+    """`iters` Gauss-Newton steps at one level; returns (R [B,3,3], t [B,3,1][, JtJ [B,6,6]]).
+    pack=True (keyword) packs eligible NCHW features first (pays off from 2 iterations)."""
     c = LevelCall(x0, x1, invD0, invD1, K, sigma0, sigma1, iters=iters, **kw)
     R, t = c.pose_buffers(pose)
     jtj = torch.empty(c.B, 6, 6, dtype=torch.float32, device=c.device) if return_jtj else None
@@ -207,7 +262,8 @@ def debug_pixels(pose, x0, x1, invD0, invD1, K, sigma0, sigma1, **kw):
     """Per-pixel dump [B,5,H,W] (u, v, sigma_r ch0, sigma0 ch0, occlusion|mask invalid) -- tests only."""
     c = LevelCall(x0, x1, invD0, invD1, K, sigma0, sigma1, iters=1, **kw)
     R, t = c.pose_buffers(pose)
-    out = torch.empty(c.B, 5, x0.shape[2], x0.shape[3], dtype=torch.float32, device=c.device)
+    _, _, H, W = feature_shape(x0)
+    out = torch.empty(c.B, 5, H, W, dtype=torch.float32, device=c.device)
     rc = N.lib().dpft_ic_debug_pixels(ctypes.byref(c.desc), ctypes.byref(c.tens), _ptr(R), _ptr(t), _ptr(out),
                                       _ptr(c.ws), c.ws_bytes, _stream(c.device))
     N.check(rc, "dpft_ic_debug_pixels")

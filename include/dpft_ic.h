@@ -57,6 +57,10 @@ extern "C" {
 #define DPFT_NO_UNCERTAINTY   0x4u /* IC tracker, TrustRegionBase (algorithms.py:23-139):
                                       sigma = 1, s0/s1 ignored (may be NULL), occluded
                                       residual 1e-3; excludes the two flags above     */
+#define DPFT_FEATURES_C4      0x8u /* f0 / f1 in channel-quad layout [B][C/4][H][W][4]
+                                      (dpft_pack_features); needs C % 4 == 0 and Cs == 1
+                                      (or NO_UNCERTAINTY).  Same values, coalesced
+                                      16-byte loads of 4 channels per pixel / tap.    */
 
 /* device status word bits */
 #define DPFT_STATUS_NONFINITE 0x1u /* a JtJ / JtR reduction was not finite         */
@@ -73,7 +77,7 @@ typedef struct DpftLevelDesc {
     int32_t Cs;      /* uncertainty channels: 1 (broadcast) or C              */
     int32_t H, W;    /* level resolution                                      */
     int32_t iters;   /* Gauss-Newton iterations (reference: max_iter_per_pyr)  */
-    uint32_t flags;  /* DPFT_REMOVE_TRU_SIGMA | DPFT_COMBINE_ICP              */
+    uint32_t flags;  /* DPFT_REMOVE_TRU_SIGMA | DPFT_COMBINE_ICP | ...        */
     float icp_weight;/* ScaleNet('None') weight, 0.01 (algorithms.py:1563)    */
 } DpftLevelDesc;
 
@@ -166,6 +170,14 @@ size_t dpft_preprocess_workspace_size(void);
 int dpft_preprocess_depth(const float* depth, int32_t B, int32_t H, int32_t W, int32_t levels,
                           float* const* invd_out, float* const* depth_out,
                           void* workspace, size_t workspace_bytes, void* hip_stream);
+
+/*
+ * Feature relayout for DPFT_FEATURES_C4: src [B,C,H,W] (NCHW, the encoder's
+ * output, LeastSquareTracking.py:679-680) -> dst [B,C/4,H,W,4], C % 4 == 0.
+ * Pose-independent: done once per level per forward, every Gauss-Newton iteration
+ * and every residual pose of the level reads the packed copy.  src != dst.
+ */
+int dpft_pack_features(const float* src, float* dst, int32_t B, int32_t C, int32_t H, int32_t W, void* hip_stream);
 
 int dpft_version(void);            /* DPFT_ABI_VERSION */
 const char* dpft_last_error(void); /* thread-local message of the last failure */

@@ -1,0 +1,152 @@
+"""Channel-quad feature layout (DPFT_FEATURES_C4) on a real MI355X (`-m gpu`).
+
+The packed layout changes only where the values live, not what is computed:
+every Gauss-Newton iteration of the C4 reduce kernel must give the pose, the
+normal equations and the invalid count of the NCHW kernel (same per-pixel
+arithmetic, channels summed in the same order), and both must match the
+reference's golden vectors within the se(3) tolerance.
+"""
+import numpy as np
+import pytest
+import torch
+
+import golden_io
+
+pytestmark = pytest.mark.gpu
+
+SE3_TOL = 1e-4
+
+
+def _dev():
+    if not torch.cuda.is_available():
+        pytest.skip("no HIP device")
+    return torch.device("cuda:0")
+
+
+def _trace(name, dev, pack):
+    from deep_prob_feature_track_amd import ic
+    case, z = golden_io.load(name)
+    lv = golden_io.levels_torch(case, torch.float32, dev)
+    R, t = golden_io.init_pose(case, torch.float32, dev)
+    t = t.view(-1, 3, 1)
+    K = torch.from_numpy(case["K"]).to(dev)
+    out = []
+    for l in reversed(range(case["levels"])):
+        d = lv[l]
+        f0, f1 = (ic.pack_features(d["f0"]), ic.pack_features(d["f1"])) if pack else (d["f0"], d["f1"])
+        for it in range(3):
+            R, t, jtj, jtr, inv = ic.iterate(
+                (R, t), f0, f1, d["invD0"], d["invD1"], K / 2 ** l, d["s0"], d["s1"], first=(it == 0),
+                remove_tru_sigma=bool(z["opt_remove_tru_sigma"]), obj_mask0=d.get("mask0"),
+                obj_mask1=d.get("mask1"), depth0=d.get("depth0"), depth1=d.get("depth1"),
+                combine_icp=bool(z["opt_combine_icp"]))
+            out.append(dict(R=R.cpu().numpy(), t=t.view(-1, 3).cpu().numpy(), jtj=jtj.cpu().numpy(),
+                            jtr=jtr.cpu().numpy(), invalid=inv.cpu().numpy()))
+    return case, z, out
+
+
+@pytest.mark.parametrize("B,C,H,W", [(2, 8, 37, 70), (1, 32, 120, 160), (3, 4, 5, 3)])
+def test_pack_round_trip_bit_exact(B, C, H, W):
+    from deep_prob_feature_track_amd import ic
+    dev = _dev()
+    x = torch.randn(B, C, H, W, device=dev)
+    p = ic.pack_features(x)
+    assert p.shape == (B, C // 4, H, W, 4)
+    ref = x.view(B, C // 4, 4, H, W).permute(0, 1, 3, 4, 2)
+    assert torch.equal(p, ref)
+    assert torch.equal(ic.unpack_features(p), x)
+
+
+@pytest.mark.parametrize("name", ["cfg1_160x120_c8", "batch4_160x120_c8", "masks_160x120_c8",
+                                  "cfg2_640x480_c32", "icp_160x120_c8"])
+def test_c4_equals_nchw_and_golden(name):
+    dev = _dev()
+    case, z, a = _trace(name, dev, pack=False)
+    _, _, b = _trace(name, dev, pack=True)
+    # Chained traces: poses drift apart by summation-order noise (the channel sums are
+    # regrouped, see ic_reduce_kernel's Q); both stay on the reference's trajectory.
+    for i, (x, y) in enumerate(zip(a, b)):
+        for prec in ("f32", "f64"):  # the contract: the reference's own trajectory within 1e-4
+            if f"{prec}_R" in z:
+                assert np.abs(y["R"] - z[f"{prec}_R"][i]).max() <= SE3_TOL, f"iter {i} vs {prec}"
+                assert np.abs(y["t"] - z[f"{prec}_t"][i]).max() <= SE3_TOL, f"iter {i} vs {prec}"
+        # between the layouts: summation-order noise (the reference's own fp32 run sits up
+        # to 9.7e-5 from its fp64 run at 640x480)
+        dR, dt = np.abs(x["R"] - y["R"]).max(), np.abs(x["t"] - y["t"]).max()
+        assert dR < 5e-5 and dt < 5e-5, f"iter {i}: |dR| {dR:.2e} |dt| {dt:.2e}"
+    assert (a[0]["invalid"] == b[0]["invalid"]).all()
+
+
+@pytest.mark.parametrize("name", ["cfg1_160x120_c8", "batch4_160x120_c8", "masks_160x120_c8",
+                                  "cfg2_640x480_c32", "icp_160x120_c8"])
+def test_c4_iteration_from_reference_pose(name):
+    """Every iteration re-started from the reference's own pose of the previous
+    iteration: both layouts give the reference's invalid count exactly and the same
+    normal equations (a chained trace cannot show this: the invalid count of these
+    cases moves by up to 3 % under 1e-5 pose noise)."""
+    from deep_prob_feature_track_amd import ic
+    dev = _dev()
+    case, z = golden_io.load(name)
+    lv = golden_io.levels_torch(case, torch.float32, dev)
+    R0, t0 = golden_io.init_pose(case, torch.float32, dev)
+    K = torch.from_numpy(case["K"]).to(dev)
+    i = 0
+    for l in reversed(range(case["levels"])):
+        d = lv[l]
+        packed = (ic.pack_features(d["f0"]), ic.pack_features(d["f1"]))
+        for it in range(3):
+            R = torch.from_numpy(z["f32_R"][i - 1]).to(dev) if i else R0
+            t = (torch.from_numpy(z["f32_t"][i - 1]).to(dev) if i else t0).reshape(-1, 3, 1)
+            out = []
+            for f0, f1 in ((d["f0"], d["f1"]), packed):
+                o = ic.iterate((R, t), f0, f1, d["invD0"], d["invD1"], K / 2 ** l, d["s0"], d["s1"], first=True,
+                               remove_tru_sigma=bool(z["opt_remove_tru_sigma"]), obj_mask0=d.get("mask0"),
+                               obj_mask1=d.get("mask1"), depth0=d.get("depth0"), depth1=d.get("depth1"),
+                               combine_icp=bool(z["opt_combine_icp"]))
+                out.append([x.cpu().numpy() for x in o])
+            (Ra, ta, ja, ra, na), (Rb, tb, jb, rb, nb) = out
+            assert (na == nb).all() and (nb == z["f32_invalid"][i]).all(), f"iter {i}: {na} {nb} {z['f32_invalid'][i]}"
+            assert np.abs(ja - jb).max() / np.abs(ja).max() < 1e-6, f"iter {i}"
+            assert np.abs(ra - rb).max() / np.abs(ra).max() < 1e-4, f"iter {i}"
+            i += 1
+
+
+@pytest.mark.parametrize("no_unc", [False, True])
+def test_c4_random_ragged_solve_and_residual(no_unc):
+    """Ragged tiles, C = 12 (a non-specialised channel count), masks, IC and U_IC."""
+    from deep_prob_feature_track_amd import ic
+    dev = _dev()
+    g = torch.Generator().manual_seed(7)
+    B, C, H, W = 2, 12, 37, 70
+    f0 = torch.rand(B, C, H, W, generator=g)
+    f1 = torch.roll(f0, shifts=(1, 2), dims=(2, 3)) + 0.01 * torch.rand(B, C, H, W, generator=g)
+    s0 = 0.5 + torch.rand(B, 1, H, W, generator=g)
+    s1 = 0.5 + torch.rand(B, 1, H, W, generator=g)
+    d0 = 0.2 + torch.rand(B, 1, H, W, generator=g)
+    d1 = 0.2 + torch.rand(B, 1, H, W, generator=g)
+    m1 = torch.rand(B, 1, H, W, generator=g) > 0.2
+    K = torch.tensor([[W * 0.8, W * 0.8, (W - 1) / 2, (H - 1) / 2]]).repeat(B, 1)
+    T = [v.to(dev) for v in (f0, f1, s0, s1, d0, d1, m1, K)]
+    f0, f1, s0, s1, d0, d1, m1, K = T
+    pose = (torch.eye(3, device=dev).repeat(B, 1, 1), torch.zeros(B, 3, 1, device=dev))
+    kw = dict(no_uncertainty=True) if no_unc else dict(remove_tru_sigma=True)
+    sa, sb = (None, None) if no_unc else (s0, s1)
+    ra = ic.solve_level(pose, f0, f1, d0, d1, K, sa, sb, iters=3, obj_mask1=m1, **kw)
+    rb = ic.solve_level(pose, f0, f1, d0, d1, K, sa, sb, iters=3, obj_mask1=m1, pack=True, **kw)
+    assert (ra[0] - rb[0]).abs().max().item() < 1e-5 and (ra[1] - rb[1]).abs().max().item() < 1e-5
+    la = ic.residual_level(pose, f0, f1, d0, d1, K, sa, sb, obj_mask1=m1, **kw)
+    lb = ic.residual_level(pose, ic.pack_features(f0), ic.pack_features(f1), d0, d1, K, sa, sb, obj_mask1=m1, **kw)
+    torch.testing.assert_close(la, lb, rtol=1e-6, atol=0)
+
+
+def test_c4_rejects_per_channel_sigma():
+    from deep_prob_feature_track_amd import ic
+    dev = _dev()
+    B, C, H, W = 1, 8, 16, 16
+    x = ic.pack_features(torch.rand(B, C, H, W, device=dev))
+    s = torch.rand(B, C, H, W, device=dev) + 0.5
+    d = torch.rand(B, 1, H, W, device=dev) + 0.2
+    K = torch.tensor([[12.0, 12.0, 7.5, 7.5]], device=dev)
+    pose = (torch.eye(3, device=dev)[None], torch.zeros(1, 3, 1, device=dev))
+    with pytest.raises(ValueError, match="single sigma plane"):
+        ic.solve_level(pose, x, x, d, d, K, s, s)
