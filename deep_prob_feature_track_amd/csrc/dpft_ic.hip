@@ -91,6 +91,22 @@ constexpr int kRowsPerStep = 4;        // one row per wave per step
 #ifndef DPFT_MIN_WAVES
 #define DPFT_MIN_WAVES 1
 #endif
+#ifndef DPFT_MARCH
+#define DPFT_MARCH 1
+#endif
+#ifndef DPFT_RING_M
+#define DPFT_RING_M 2
+#endif
+constexpr bool kMarch = DPFT_MARCH != 0;  // channel-quad reduce: row-marching window (1) or 4-row tiles (0)
+#ifndef DPFT_WGMARCH
+#define DPFT_WGMARCH 0
+#endif
+constexpr bool kWgMarch = DPFT_WGMARCH != 0;  // channel-quad U_IC / IC: workgroup-marching kernel
+constexpr int kRingM = DPFT_RING_M;       // quads in flight on the marching path (kRingM - 1 ahead)
+#ifndef DPFT_F0_AUX
+#define DPFT_F0_AUX 2
+#endif
+constexpr int kF0Aux = DPFT_F0_AUX;       // cache policy of the marching f0 stream (2: nt)
 constexpr int kCK = DPFT_CK;           // channels per pipeline unit
 constexpr int kRing = DPFT_RING;       // load slots in flight ring (kRing - 1 units ahead)
 constexpr int kRPL = DPFT_RPL;         // image rows per lane (Cs == 1 kernels)
@@ -1019,11 +1035,13 @@ template <int CT, bool CS1, bool TRU, int MODE, bool C4>
 __global__ __launch_bounds__(kThreads, DPFT_MIN_WAVES) void ic_reduce_kernel(IterParams p) {
   constexpr bool ICP = MODE == 1, NOSIG = MODE == 2;
   static_assert(!C4 || CS1, "the channel-quad layout needs one sigma plane");
-  constexpr int R = C4 ? kRPL4 : (CS1 ? kRPL : 1);  // rows per lane
+  constexpr int R = C4 ? ((kMarch && CT > 0) ? 1 : kRPL4) : (CS1 ? kRPL : 1);  // rows per lane
   constexpr float kFill = NOSIG ? 1e-3f : 1e-6f;  // weighted residual of invalid pixels
   const int C = CT > 0 ? CT : p.C;
   __shared__ float lds_ext[TRU ? 2 * 7 : 1][kThreads];  // extremum corrections (6 + count), min then max
   __shared__ float red[4][kRec];
+  constexpr bool kWin = C4 && kMarch && CT > 0;
+  __shared__ f32x4 lds_win[kWin ? 4 : 1][kWin ? 2 * (CT / 4) * 64 : 1];
 
   const int tid = threadIdx.x, lane = tid & 63, wave = wave_id();
   const int W = p.W, H = p.H, HW = H * W;
@@ -1103,9 +1121,8 @@ __global__ __launch_bounds__(kThreads, DPFT_MIN_WAVES) void ic_reduce_kernel(Ite
     for (int r = 0; r < R; ++r) dv[r] = bld(rd0, min(y0 + r, H - 1) * W * 4 + min(max(xs, 0), W - 1) * 4, 0);
   };
   // frame of tile `it` from its inverse depths; issues the frame's gathers (consumed by pixel_terms)
-  auto make_frame = [&](int it, const float (&dv)[R], Frame& F) {
-    int xs;
-    tile_pos(it, xs, F.y0);
+  auto make_frame_xy = [&](int xs, int y0, const float (&dv)[R], Frame& F, bool s0_rows) {
+    F.y0 = y0;
     F.xc = min(max(xs, 0), W - 1);  // clamped: replicate padding of the stencil
     F.out_lane = (lane >= 1) && (lane <= kTileOut) && (xs < W);
     F.colv = F.xc * 4;
@@ -1125,10 +1142,15 @@ __global__ __launch_bounds__(kThreads, DPFT_MIN_WAVES) void ic_reduce_kernel(Ite
       F.m1[r] = m1b ? bil_u8(m1b, F.tp[r]) : 1.0f;
       if (CS1 && !NOSIG) F.gs1[r] = gather4(rs1, F.tp[r], 0);
     }
-    if (CS1 && !NOSIG) {
+    if (CS1 && !NOSIG && s0_rows) {
 #pragma unroll
       for (int j = 0; j < R + 2; ++j) F.s0r[j] = bld(rs0, F.colv, F.rows[j]);
     }
+  };
+  auto make_frame = [&](int it, const float (&dv)[R], Frame& F) {
+    int xs, y0;
+    tile_pos(it, xs, y0);
+    make_frame_xy(xs, y0, dv, F, true);
   };
 
   // per-pixel occlusion / uncertainty terms of a frame (one sigma plane: before or after the channels)
@@ -1238,7 +1260,180 @@ __global__ __launch_bounds__(kThreads, DPFT_MIN_WAVES) void ic_reduce_kernel(Ite
     }
   };
 
-  if constexpr (C4) {
+  if constexpr (C4 && kMarch && CT > 0) {
+    // ---- channel-quad layout, row-marching register window.  Each WAVE owns a
+    // contiguous run of (column strip, row) units of its pair, strip-major, and walks
+    // it row by row keeping the f0 rows y - dir and y of every quad (and of sigma0) in
+    // registers: per row and quad it loads only row y + dir of f0 plus the f1 taps,
+    // so every f0 / sigma0 row comes from HBM once per band instead of three times
+    // (the tile path re-reads the halo rows after L2 has dropped them).  Odd waves
+    // march upwards, so the two waves that share a band boundary reach it at the same
+    // time (at the start, or at the end) and its halo rows / tap rows hit in L2.
+    // The per-pixel weights factor out of the channel sums exactly as on the tile path.
+    constexpr int NQ = CT / 4;
+    static_assert(CT % 4 == 0, "channel quads");
+    const int U = p.tiles_x * H;
+    const int nw = p.nbpp * 4, jw = jb * 4 + wave;
+    const int ubeg = (int)(((long)U * jw) / nw), uend = (int)(((long)U * (jw + 1)) / nw);
+    const int nrows = uend - ubeg;
+    const bool up = (jw & 1) != 0;
+    const int dir = up ? -1 : 1;
+    const float dirf = up ? -1.0f : 1.0f;
+    const int row_restart = up ? H - 1 : 0;  // a strip begins here in marching order
+    auto unit_pos = [&](int k, int& xs, int& y) {
+      const int u = up ? uend - 1 - k : ubeg + k;
+      const int strip = u / H;
+      y = u - strip * H;
+      xs = strip * kTileOut - 1 + lane;
+    };
+    // window in LDS, per wave [2 slots][NQ quads][64 lanes]: at row step k slot k & 1 holds
+    // row y - dir and slot (k + 1) & 1 row y; the new row y + dir overwrites the first slot
+    // right after this lane has read it (each lane only ever touches its own column, and a
+    // wave's LDS accesses complete in order: no barrier)
+    f32x4* win = lds_win[wave];
+    float sprev = 0.f, scur = 0.f;
+    struct QuadM {
+      f32x4 f;      // f0 row y + dir
+      f32x4 t[4];   // f1 taps (see gather4 / QuadLoadsR)
+    };
+    float d_cur[1] = {0.f};
+    if (nrows > 0) {
+      int xs, y;
+      unit_pos(0, xs, y);
+      d_cur[0] = bld(rd0, y * W * 4 + min(max(xs, 0), W - 1) * 4, 0);
+    }
+    for (int k = 0; k < nrows; ++k) {
+      int xs, y;
+      unit_pos(k, xs, y);
+      const float dv[1] = {d_cur[0]};
+      if (k + 1 < nrows) {
+        int xn, yn;
+        unit_pos(k + 1, xn, yn);
+        d_cur[0] = bld(rd0, yn * W * 4 + min(max(xn, 0), W - 1) * 4, 0);
+      }
+      const int colq = min(max(xs, 0), W - 1) * 16;
+      if (k == 0 || y == row_restart) {  // prime the window: rows y - dir (replicate-clamped) and y
+        const int yp = min(max(y - dir, 0), H - 1);
+#pragma unroll
+        for (int q = 0; q < NQ; ++q) {
+          win[((k & 1) * NQ + q) * 64 + lane] = llvm_buf_load_f32x4(rf0, colq, q * 4 * (int)planeB + yp * W * 16, kF0Aux);
+          win[(((k + 1) & 1) * NQ + q) * 64 + lane] = llvm_buf_load_f32x4(rf0, colq, q * 4 * (int)planeB + y * W * 16, kF0Aux);
+        }
+        if (CS1 && !NOSIG) {
+          sprev = bld(rs0, colq >> 2, yp * W * 4);
+          scur = bld(rs0, colq >> 2, y * W * 4);
+        }
+      }
+      const int yn = min(max(y + dir, 0), H - 1);
+      Frame F;
+      make_frame_xy(xs, y, dv, F, false);
+      float snew = 0.f;
+      if (CS1 && !NOSIG) snew = bld(rs0, colq >> 2, yn * W * 4);
+      QuadM L[kRingM];
+      auto issue = [&](QuadM& Q, int q) {
+#if DPFT_ABL == 1  // profiling ablation: no channel loop (frame + epilogue only)
+        return;
+#endif
+        const int po = q * 4 * (int)planeB;
+        Q.f = llvm_buf_load_f32x4(rf0, colq, po + yn * W * 16, kF0Aux);
+#if DPFT_ABL == 3  // profiling ablation: no f1 gathers
+        Q.t[0] = Q.t[1] = Q.t[2] = Q.t[3] = Q.f;
+#else
+        Q.t[0] = bld4(rf1, F.tp[0].ob0 * 16, po);
+        Q.t[1] = bld4(rf1, F.tp[0].ob0 * 16 + 16, po);
+        Q.t[2] = bld4(rf1, F.tp[0].ob1 * 16, po);
+        Q.t[3] = bld4(rf1, F.tp[0].ob1 * 16 + 16, po);
+#endif
+      };
+#pragma unroll
+      for (int q = 0; q + 1 < kRingM; ++q)
+        if (q < NQ) issue(L[q], q);
+      if (CS1 && !NOSIG) {
+        F.s0r[0] = up ? snew : sprev;
+        F.s0r[1] = scur;
+        F.s0r[2] = up ? sprev : snew;
+        sprev = scur;
+        scur = snew;
+      }
+      PixelTerms T;
+      pixel_terms(F, T);
+      f32x2 Q[9];
+#pragma unroll
+      for (int i = 0; i < 9; ++i) Q[i] = f32x2{0.f, 0.f};
+      const PairWeights& w = F.pw[0];
+      static_assert(NQ % kRingM == 0, "quads per ring round");
+      auto quad = [&](int q, const QuadM& cur) {
+#if DPFT_ABL == 1
+        return;
+#endif
+        f32x4* sp = win + ((k & 1) * NQ + q) * 64 + lane;
+        const f32x4 wp = *sp, wc = win[(((k + 1) & 1) * NQ + q) * 64 + lane];
+#if DPFT_ABL == 2  // profiling ablation: loads only
+        {
+          const f32x4 z = wp + wc + cur.f + cur.t[0] + cur.t[1] + cur.t[2] + cur.t[3];
+          Q[0] += f32x2{z.x, z.y};
+          Q[1] += f32x2{z.z, z.w};
+          *sp = cur.f;
+          return;
+        }
+#endif
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {  // channels 4q + 2h, 4q + 2h + 1
+          auto half = [&](const f32x4& v) { return h ? f32x2{v.z, v.w} : f32x2{v.x, v.y}; };
+          const f32x2 fp = half(wp), fm = half(wc), fn = half(cur.f);
+          const f32x2 V = (fp + fn) + 2.0f * fm;
+          const f32x2 D = (fn - fp) * dirf;  // bottom - top
+          const f32x2 x = f32x2{lane_from_right(V.x) - lane_from_left(V.x), lane_from_right(V.y) - lane_from_left(V.y)};
+          const f32x2 yv =
+              f32x2{lane_from_left(D.x) + lane_from_right(D.x), lane_from_left(D.y) + lane_from_right(D.y)} + 2.0f * D;
+          const f32x2 n2 = x * x + yv * yv + 1e-8f;
+          const f32x2 inv = f32x2{__builtin_amdgcn_rsqf(n2.x), __builtin_amdgcn_rsqf(n2.y)};
+          const f32x2 gx = x * inv, gy = yv * inv;
+          const f32x2 res = (half(cur.t[0]) * w.w0 + half(cur.t[1]) * w.w1 + half(cur.t[2]) * w.w2 +
+                             half(cur.t[3]) * w.w3) - fm;
+          Q[0] += gx * gx;
+          Q[1] += gx * gy;
+          Q[2] += gy * gy;
+          Q[3] += gx * res;
+          Q[4] += gy * res;
+          Q[5] += res * res;
+          Q[6] += gx;
+          Q[7] += gy;
+          Q[8] += res;
+        }
+        *sp = cur.f;
+      };
+      // every ring round but the last refills unconditionally: each load set keeps its registers
+#pragma unroll 1
+      for (int q0 = 0; q0 < NQ - kRingM; q0 += kRingM) {
+#pragma unroll
+        for (int qq = 0; qq < kRingM; ++qq) {
+          issue(L[(qq + kRingM - 1) % kRingM], q0 + qq + kRingM - 1);
+          quad(q0 + qq, L[qq]);
+        }
+      }
+#pragma unroll
+      for (int qq = 0; qq < kRingM; ++qq) {
+        if (qq == 0) issue(L[kRingM - 1], NQ - 1);
+        quad(NQ - kRingM + qq, L[qq]);
+      }
+      Sums S;
+      {
+        float q[9];
+#pragma unroll
+        for (int i = 0; i < 9; ++i) q[i] = Q[i].x + Q[i].y;
+        const float A = T.inv_s[0], bx = T.kk[0] * T.hx[0], by = T.kk[0] * T.hy[0], A2 = A * A;
+        S.Saa[0] = A2 * q[0] + 2.0f * A * bx * q[3] + bx * bx * q[5];
+        S.Sab[0] = A2 * q[1] + A * by * q[3] + A * bx * q[4] + bx * by * q[5];
+        S.Sbb[0] = A2 * q[2] + 2.0f * A * by * q[4] + by * by * q[5];
+        S.Sa[0] = A * q[6] + bx * q[8];
+        S.Sb[0] = A * q[7] + by * q[8];
+        S.Sar[0] = A2 * q[3] + A * bx * q[5];
+        S.Sbr[0] = A2 * q[4] + A * by * q[5];
+      }
+      finish_pixels(F, T, S);
+    }
+  } else if constexpr (C4) {
     // ---- channel-quad layout: the per-pixel weights factor out of the channel sums
     // (alpha = 1/sigma, bx = kk hx, by = kk hy give na = alpha gx + bx r,
     // nb = alpha gy + by r, rw = alpha r for every channel), so the channel loop needs
@@ -1524,6 +1719,369 @@ __global__ __launch_bounds__(kThreads, DPFT_MIN_WAVES) void ic_reduce_kernel(Ite
   }
 }
 
+// ============================================================ workgroup-marching reduce kernel
+// Channel-quad layout, one sigma plane, U_IC (MODE 0) or IC (MODE 2), C % 16 == 0.
+// A WORKGROUP owns a contiguous run of (column strip, row) units of its pair and
+// marches it row by row; its 4 waves split the channel quads of every row (wave w:
+// quads w*QW .. w*QW+QW-1), so one workgroup-row moves all channels in a quarter of
+// the time a single wave needs and only ~2 workgroups per CU are in flight: the f1
+// tap rows a row shares with the next one are still in L2 when the next row asks
+// (each f1 row comes from HBM ~once; the per-wave march re-fetched it, 1.55x), and f0
+// comes from HBM once through a per-wave register window of rows y - dir, y.
+// Per row only ONE wave computes the warp / taps / occlusion / sigma terms (the wave
+// ((m - 2) & 3) for row m, two rows ahead) and publishes them in LDS; the channel
+// loads of row m + 1 are issued before row m is computed (two row buffers), and the
+// four waves' channel sums meet in LDS behind one barrier per row.  Every wave then
+// forms the per-pixel sums S and accumulates its own share of the 27 normal-equation
+// entries (wave 3: JtR, invalid count and the truncated-sigma extrema).
+template <int W_>
+struct WaveIdx {
+  static constexpr int value = W_;
+};
+
+template <int CT, bool TRU, int MODE>
+__global__ __launch_bounds__(kThreads, 2) void ic_wgmarch_kernel(IterParams p) {
+  constexpr bool NOSIG = MODE == 2;
+  static_assert(MODE != 1, "combine_ICP runs on ic_reduce_kernel");
+  constexpr int NQ = CT / 4, QW = NQ / 4;
+  static_assert(CT % 16 == 0 && QW >= 1, "4 waves x whole channel quads");
+  constexpr float kFill = NOSIG ? 1e-3f : 1e-6f;
+  // frame slot fields (per lane): tap pair bases, pair weights, inverse depth, pixel terms
+  enum { F_OB0, F_OB1, F_W0, F_W1, F_W2, F_W3, F_D, F_A, F_BX, F_BY, F_INV, F_SR0, kSlotF };
+  __shared__ float fr[4][kSlotF][64];
+  __shared__ float qs[2][4][9][64];
+  __shared__ float lds_ext[TRU ? 14 : 1][64];
+  __shared__ float red[kRec];
+
+  const int lane = threadIdx.x & 63, wave = wave_id();
+  const int W = p.W, H = p.H;
+  const int kb = xcd_remap(blockIdx.x, gridDim.x);
+  const int b = kb / p.nbpp, jb = kb - b * p.nbpp;
+  const int U = p.tiles_x * H;
+  const int ubeg = (int)(((long)U * jb) / p.nbpp), uend = (int)(((long)U * (jb + 1)) / p.nbpp);
+  const bool up = (jb & 1) != 0;  // odd workgroups march upwards: shared band boundaries meet in time
+  const int dir = up ? -1 : 1;
+  const float dirf = up ? -1.0f : 1.0f;
+  const float g0min = TRU ? dec_ord(p.ext[0]) : 0.f, g0max = TRU ? dec_ord(p.ext[1]) : 0.f;
+  const uint32_t planeB = (uint32_t)(H * W) * 4u;
+  const int HW = H * W;
+
+  const float fx = p.K[4 * b + 0], fy = p.K[4 * b + 1], cx = p.K[4 * b + 2], cy = p.K[4 * b + 3];
+  float Rm[9], tv[3];
+#pragma unroll
+  for (int k = 0; k < 9; ++k) Rm[k] = p.R[9 * b + k];
+#pragma unroll
+  for (int k = 0; k < 3; ++k) tv[k] = p.t[3 * b + k];
+
+  const auto rf0 = rsrc(p.f0 + (size_t)b * CT * HW, planeB * CT);
+  const auto rf1 = rsrc(p.f1 + (size_t)b * CT * HW, planeB * CT);
+  const auto rs0 = rsrc(NOSIG ? p.invD0 : p.s0 + (size_t)b * HW, planeB);
+  const auto rs1 = rsrc(NOSIG ? p.invD0 : p.s1 + (size_t)b * HW, planeB);
+  const auto rd0 = rsrc(p.invD0 + (size_t)b * HW, planeB);
+  const auto rd1 = rsrc(p.invD1 + (size_t)b * HW, planeB);
+  const uint8_t* m0b = p.mask0 ? p.mask0 + (size_t)b * HW : nullptr;
+  const uint8_t* m1b = p.mask1 ? p.mask1 + (size_t)b * HW : nullptr;
+
+  float accw[7];
+#pragma unroll
+  for (int i = 0; i < 7; ++i) accw[i] = 0.0f;
+  float mn_all = INFINITY, mn0 = INFINITY, mx_all = -INFINITY, mx0 = -INFINITY;
+  if (TRU && wave == 3) {
+#pragma unroll
+    for (int i = 0; i < 14; ++i) lds_ext[i][lane] = 0.0f;
+  }
+
+  struct RowLoads {
+    f32x4 f[QW];     // f0 row y + dir of this wave's quads
+    f32x4 t[QW][4];  // f1 taps (pair bases, see gather4)
+  };
+  RowLoads L[2];
+  f32x4 wprev[QW], wcur[QW];
+
+  // segments: the unit range split at strip boundaries, walked in marching order
+  const int s_first = ubeg / H, s_last = (uend - 1) / H;
+  for (int si = 0; si <= s_last - s_first; ++si) {
+    const int strip = up ? s_last - si : s_first + si;
+    const int ya = max(ubeg - strip * H, 0), yb = min(uend - strip * H, H);
+    const int n = yb - ya;
+    if (n <= 0) continue;
+    __syncthreads();  // the previous segment's last row may still be reading frame slot 0
+    auto yrow = [&](int m) { return up ? yb - 1 - m : ya + m; };
+    const int xs = strip * kTileOut - 1 + lane;
+    const int xc = min(max(xs, 0), W - 1);
+    const bool out_lane = (lane >= 1) && (lane <= kTileOut) && (xs < W);
+    const int colq = xc * 16;
+
+    // frame-wave state: wave w frames rows m = w + 2 (mod 4), two steps ahead
+    float dpre = 0.f;
+    {
+      const int mf = (wave + 2) & 3;
+      if (mf < n) dpre = bld(rd0, yrow(mf) * W * 4 + xc * 4, 0);
+    }
+    // one pipeline step: row k + 2 framed, row k + 1 loaded, row k reduced.  P = k & 1 is a
+    // template constant so the two row buffers stay in registers (a runtime index would
+    // put them in scratch).
+    auto step = [&](int k, auto PC) {
+      constexpr int P = decltype(PC)::value;
+      const bool framer = ((k & 3) == wave) && (k + 2 < n);
+      // ---- P1: warp / taps of row k + 2, its gathers (issued before this step's channel loads)
+      Warp fw;
+      PairWeights fpw;
+      Gather4 gd1, gs1;
+      float s0t = 0.f, s0m = 0.f, s0b = 0.f, fm1 = 1.0f;
+      bool fm0 = true;
+      if (framer) {
+        const int m = k + 2, y = yrow(m);
+        const float d = dpre;
+        fw = warp_point(xc, y, d, Rm, tv, fx, fy, cx, cy);
+        const Taps tp = make_taps(fw.u, fw.v, H, W);
+        fpw = pair_weights(tp);
+        gd1 = gather4(rd1, tp, 0);
+        if (!NOSIG) {
+          gs1 = gather4(rs1, tp, 0);
+          s0t = bld(rs0, xc * 4, max(y - 1, 0) * W * 4);
+          s0m = bld(rs0, xc * 4, y * W * 4);
+          s0b = bld(rs0, xc * 4, min(y + 1, H - 1) * W * 4);
+        }
+        if (m0b) fm0 = m0b[y * W + xc] != 0;
+        if (m1b) fm1 = bil_u8(m1b, tp);
+        if (m + 4 < n) dpre = bld(rd0, yrow(m + 4) * W * 4 + xc * 4, 0);
+        float* s = &fr[m & 3][0][lane];
+        s[F_OB0 * 64] = __int_as_float(tp.ob0);
+        s[F_OB1 * 64] = __int_as_float(tp.ob1);
+        s[F_W0 * 64] = fpw.w0;
+        s[F_W1 * 64] = fpw.w1;
+        s[F_W2 * 64] = fpw.w2;
+        s[F_W3 * 64] = fpw.w3;
+        s[F_D * 64] = d;
+      }
+      // ---- P2: channel loads of row k + 1 (this wave's quads), window prime at the segment start
+      if (k + 1 >= 0 && k + 1 < n) {
+        const int m = k + 1, y = yrow(m);
+        const int ob0 = __float_as_int(fr[m & 3][F_OB0][lane]), ob1 = __float_as_int(fr[m & 3][F_OB1][lane]);
+        if (m == 0) {
+          const int yp = min(max(y - dir, 0), H - 1);
+#pragma unroll
+          for (int qq = 0; qq < QW; ++qq) {
+            const int po = (wave * QW + qq) * 4 * (int)planeB;
+            wprev[qq] = llvm_buf_load_f32x4(rf0, colq, po + yp * W * 16, kF0Aux);
+            wcur[qq] = llvm_buf_load_f32x4(rf0, colq, po + y * W * 16, kF0Aux);
+          }
+        }
+        const int yn = min(max(y + dir, 0), H - 1);
+        RowLoads& Ld = L[1 - P];
+#pragma unroll
+        for (int qq = 0; qq < QW; ++qq) {
+          const int po = (wave * QW + qq) * 4 * (int)planeB;
+          Ld.f[qq] = llvm_buf_load_f32x4(rf0, colq, po + yn * W * 16, kF0Aux);
+          Ld.t[qq][0] = bld4(rf1, ob0 * 16, po);
+          Ld.t[qq][1] = bld4(rf1, ob0 * 16 + 16, po);
+          Ld.t[qq][2] = bld4(rf1, ob1 * 16, po);
+          Ld.t[qq][3] = bld4(rf1, ob1 * 16 + 16, po);
+        }
+      }
+      // ---- P3: channel sums of row k over this wave's quads -> LDS
+      if (k >= 0) {
+        const RowLoads& Ld = L[P];
+        const float w0 = fr[k & 3][F_W0][lane], w1 = fr[k & 3][F_W1][lane], w2 = fr[k & 3][F_W2][lane],
+                    w3 = fr[k & 3][F_W3][lane];
+        f32x2 Q[9];
+#pragma unroll
+        for (int i = 0; i < 9; ++i) Q[i] = f32x2{0.f, 0.f};
+#pragma unroll
+        for (int qq = 0; qq < QW; ++qq) {
+#pragma unroll
+          for (int h = 0; h < 2; ++h) {
+            auto half = [&](const f32x4& v) { return h ? f32x2{v.z, v.w} : f32x2{v.x, v.y}; };
+            const f32x2 fp = half(wprev[qq]), fm = half(wcur[qq]), fn = half(Ld.f[qq]);
+            const f32x2 V = (fp + fn) + 2.0f * fm;
+            const f32x2 D = (fn - fp) * dirf;  // bottom - top
+            const f32x2 x = f32x2{lane_from_right(V.x) - lane_from_left(V.x), lane_from_right(V.y) - lane_from_left(V.y)};
+            const f32x2 yv =
+                f32x2{lane_from_left(D.x) + lane_from_right(D.x), lane_from_left(D.y) + lane_from_right(D.y)} + 2.0f * D;
+            const f32x2 n2 = x * x + yv * yv + 1e-8f;
+            const f32x2 inv = f32x2{__builtin_amdgcn_rsqf(n2.x), __builtin_amdgcn_rsqf(n2.y)};
+            const f32x2 gx = x * inv, gy = yv * inv;
+            const f32x2 res =
+                (half(Ld.t[qq][0]) * w0 + half(Ld.t[qq][1]) * w1 + half(Ld.t[qq][2]) * w2 + half(Ld.t[qq][3]) * w3) - fm;
+            Q[0] += gx * gx;
+            Q[1] += gx * gy;
+            Q[2] += gy * gy;
+            Q[3] += gx * res;
+            Q[4] += gy * res;
+            Q[5] += res * res;
+            Q[6] += gx;
+            Q[7] += gy;
+            Q[8] += res;
+          }
+          wprev[qq] = wcur[qq];
+          wcur[qq] = Ld.f[qq];
+        }
+#pragma unroll
+        for (int i = 0; i < 9; ++i) qs[P][wave][i][lane] = Q[i].x + Q[i].y;
+      }
+      // ---- P5: occlusion / mask / sigma terms of row k + 2 (its gathers are older than
+      // this step's channel loads: no extra wait)
+      if (framer) {
+        const int m = k + 2;
+        const float d1w = bilp(gd1, fpw);
+        const bool ok = (fw.iz > d1w - 0.1f) && (fw.u > 0.0f) && (fw.u < (float)W) && (fw.v > 0.0f) &&
+                        (fw.v < (float)H);
+        bool invalid = !ok || !out_lane || !fm0 || !(fm1 > 0.0f);
+        float A = 1.0f, bx = 0.0f, by = 0.0f, sr0 = 0.0f;
+        if (!NOSIG) {
+          float hx, hy;
+          sobel_cols(s0t, s0m, s0b, hx, hy);
+          sr0 = bilp(gs1, fpw);
+          const float sg = sqrtf(sr0 * sr0 + s0m * s0m);
+          A = __builtin_amdgcn_rcpf(sg);
+          const float kk = s0m * (A * A * A);
+          bx = kk * hx;
+          by = kk * hy;
+          if (TRU) invalid = invalid || (s0m == g0min) || (s0m == g0max);
+        }
+        float* s = &fr[m & 3][0][lane];
+        s[F_A * 64] = A;
+        s[F_BX * 64] = bx;
+        s[F_BY * 64] = by;
+        s[F_INV * 64] = invalid ? 1.0f : 0.0f;
+        s[F_SR0 * 64] = sr0;
+      }
+      __syncthreads();
+      // ---- P7: per-pixel sums and this wave's share of the normal equations of row k
+      if (k >= 0 && out_lane) {
+        float q[9];
+#pragma unroll
+        for (int i = 0; i < 9; ++i)
+          q[i] = ((qs[P][0][i][lane] + qs[P][1][i][lane]) + qs[P][2][i][lane]) + qs[P][3][i][lane];
+        const float* s = &fr[k & 3][0][lane];
+        const float A = s[F_A * 64], bx = s[F_BX * 64], by = s[F_BY * 64], d = s[F_D * 64];
+        const bool invalid = s[F_INV * 64] != 0.0f;
+        const float A2 = A * A;
+        const float Saa = A2 * q[0] + 2.0f * A * bx * q[3] + bx * bx * q[5];
+        const float Sab = A2 * q[1] + A * by * q[3] + A * bx * q[4] + bx * by * q[5];
+        const float Sbb = A2 * q[2] + 2.0f * A * by * q[4] + by * by * q[5];
+        const float Sa = -(A * q[6] + bx * q[8]), Sb = -(A * q[7] + by * q[8]);
+        const float Sar = -(A2 * q[3] + A * bx * q[5]), Sbr = -(A2 * q[4] + A * by * q[5]);
+        float xr, yr;
+        {
+#pragma clang fp contract(off)
+          xr = ((float)xc - cx) / fx;
+          yr = ((float)yrow(k) - cy) / fy;
+        }
+        float Jx[6], Jy[6];
+        warp_jac(xr, yr, d, fx, fy, Jx, Jy);
+        auto share = [&](auto WV) {
+          constexpr int w = decltype(WV)::value;
+          if constexpr (w < 3) {  // JtJ entries 7w .. 7w + 6 (upper triangle, row-major)
+            int kq = 0;
+#pragma unroll
+            for (int i = 0; i < 6; ++i) {
+              const float Pi = Saa * Jx[i] + Sab * Jy[i], Qi = Sab * Jx[i] + Sbb * Jy[i];
+#pragma unroll
+              for (int j = i; j < 6; ++j) {
+                if (kq >= 7 * w && kq < 7 * w + 7) accw[kq - 7 * w] += Pi * Jx[j] + Qi * Jy[j];
+                ++kq;
+              }
+            }
+          } else {  // JtR (weighted residual of invalid pixels = kFill on every channel), invalid count
+            const float cA = invalid ? kFill * Sa : Sar;
+            const float cB = invalid ? kFill * Sb : Sbr;
+#pragma unroll
+            for (int i = 0; i < 6; ++i) accw[i] -= cA * Jx[i] + cB * Jy[i];
+            accw[6] += invalid ? 1.0f : 0.0f;
+            if (TRU) {
+              const float sr = s[F_SR0 * 64];
+              mn_all = fminf(mn_all, sr);
+              mx_all = fmaxf(mx_all, sr);
+              const bool le = sr <= mn0, ge = sr >= mx0;
+              if (le || ge) {
+                float corr[7];
+                const float dA = invalid ? 0.0f : (1e-6f * Sa - Sar);
+                const float dB = invalid ? 0.0f : (1e-6f * Sb - Sbr);
+#pragma unroll
+                for (int i = 0; i < 6; ++i) corr[i] = -(dA * Jx[i] + dB * Jy[i]);
+                corr[6] = invalid ? 0.0f : 1.0f;
+                if (le) {
+                  const bool reset = sr < mn0;
+                  mn0 = sr;
+#pragma unroll
+                  for (int i = 0; i < 7; ++i) lds_ext[i][lane] = (reset ? 0.0f : lds_ext[i][lane]) + corr[i];
+                }
+                if (ge) {
+                  const bool reset = sr > mx0;
+                  mx0 = sr;
+#pragma unroll
+                  for (int i = 0; i < 7; ++i)
+                    lds_ext[7 + i][lane] = (reset ? 0.0f : lds_ext[7 + i][lane]) + corr[i];
+                }
+              }
+            }
+          }
+        };
+        switch (wave) {
+          case 0: share(WaveIdx<0>{}); break;
+          case 1: share(WaveIdx<1>{}); break;
+          case 2: share(WaveIdx<2>{}); break;
+          default: share(WaveIdx<3>{}); break;
+        }
+      }
+    };
+    for (int k = -2; k < n; k += 2) {
+      step(k, WaveIdx<0>{});
+      if (k + 1 < n) step(k + 1, WaveIdx<1>{});
+    }
+  }
+
+  // ---- workgroup record: wave w holds entries 7w .. 7w + 6 (wave 3: JtR + invalid count)
+#pragma unroll
+  for (int i = 0; i < 7; ++i) {
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) accw[i] += __shfl_xor(accw[i], off);
+  }
+  if (lane == 0) {
+#pragma unroll
+    for (int i = 0; i < 7; ++i) red[7 * wave + i] = accw[i];
+  }
+  if (TRU && wave == 3) {
+    Extremum emn, emx;
+    emn.all = mn_all;
+    emn.v0 = mn0;
+    emx.all = mx_all;
+    emx.v0 = mx0;
+#pragma unroll
+    for (int i = 0; i < 6; ++i) {
+      emn.c[i] = lds_ext[i][lane];
+      emx.c[i] = lds_ext[7 + i][lane];
+    }
+    emn.n = lds_ext[6][lane];
+    emx.n = lds_ext[13][lane];
+    ext_wave_reduce<true>(emn);
+    ext_wave_reduce<false>(emx);
+    if (lane == 0) {
+      red[R_MN_ALL] = emn.all;
+      red[R_MN0] = emn.v0;
+      red[R_NMN] = emn.n;
+      red[R_MX_ALL] = emx.all;
+      red[R_MX0] = emx.v0;
+      red[R_NMX] = emx.n;
+#pragma unroll
+      for (int i = 0; i < 6; ++i) {
+        red[R_CMN + i] = emn.c[i];
+        red[R_CMX + i] = emx.c[i];
+      }
+    }
+  }
+  __syncthreads();
+  float* out = p.rec + (size_t)kb * kRec;
+  const int tid = threadIdx.x;
+  if (tid < (TRU ? R_NMX + 1 : R_NINV + 1)) st_ag(out + tid, red[tid]);
+  if (p.fin_on && block_is_last(p.fin.pair_cnt + b, 1u, (uint32_t)p.nbpp)) {
+    pair_reduce(p.fin, b);
+    if (block_is_last(p.fin.done_cnt, 1u, (uint32_t)p.B)) finalize_batch(p.fin);
+  }
+}
+
 // ============================================================ residual-only kernel
 // blockIdx.y = pose index: P poses per pair share the level's inputs; pose p
 // evaluates the batch of B pairs at R[p], t[p] (its own batch-global
@@ -1688,11 +2246,36 @@ __global__ __launch_bounds__(kThreads) void minmax_kernel(const float* __restric
                                                           int slot) {
   __shared__ float sm[2][4];
   float mn = INFINITY, mx = -INFINITY;
+  // 16-byte loads, four in flight per thread per round (a scalar grid-stride loop
+  // waits one memory latency per element: 17.6 us for 9.8 MB at level 0)
+  const size_t head = std::min<size_t>(((16 - (reinterpret_cast<uintptr_t>(s) & 15)) & 15) / 4, n);
+  const size_t n4 = (n - head) / 4;
+  const f32x4* s4 = reinterpret_cast<const f32x4*>(s + head);
   const size_t stride = (size_t)gridDim.x * kThreads;
-  for (size_t i = (size_t)blockIdx.x * kThreads + threadIdx.x; i < n; i += stride) {
-    const float v = s[i];
-    mn = fminf(mn, v);
-    mx = fmaxf(mx, v);
+  const size_t t0 = (size_t)blockIdx.x * kThreads + threadIdx.x;
+  size_t i = t0;
+  for (; i + 3 * stride < n4; i += 4 * stride) {
+    f32x4 v[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) v[u] = __builtin_nontemporal_load(s4 + i + u * stride);
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      mn = fminf(mn, fminf(fminf(v[u].x, v[u].y), fminf(v[u].z, v[u].w)));
+      mx = fmaxf(mx, fmaxf(fmaxf(v[u].x, v[u].y), fmaxf(v[u].z, v[u].w)));
+    }
+  }
+  for (; i < n4; i += stride) {
+    const f32x4 v = s4[i];
+    mn = fminf(mn, fminf(fminf(v.x, v.y), fminf(v.z, v.w)));
+    mx = fmaxf(mx, fmaxf(fmaxf(v.x, v.y), fmaxf(v.z, v.w)));
+  }
+  if (t0 < head) {  // unaligned head
+    mn = fminf(mn, s[t0]);
+    mx = fmaxf(mx, s[t0]);
+  }
+  for (size_t j = head + n4 * 4 + t0; j < n; j += stride) {  // tail
+    mn = fminf(mn, s[j]);
+    mx = fmaxf(mx, s[j]);
   }
   for (int off = 32; off > 0; off >>= 1) {
     mn = fminf(mn, __shfl_xor(mn, off));
@@ -2000,7 +2583,12 @@ int launch_reduce_k(IterParams p, hipStream_t st) {
   const void* k = reinterpret_cast<const void*>(&ic_reduce_kernel<CT, CS1, TRU, MODE, C4>);
   const int cap = resident_blocks(k);
   if (cap <= 0) return fail(DPFT_E_HIP, "occupancy query failed");
-  p.nbpp = std::max(1, std::min(cap / p.B, p.per_pair));
+#ifdef DPFT_GRID_DIV
+  const int capd = cap / DPFT_GRID_DIV;
+#else
+  const int capd = cap;
+#endif
+  p.nbpp = std::max(1, std::min(capd / p.B, p.per_pair));
   p.fin.nbpp = p.nbpp;
   hipLaunchKernelGGL((ic_reduce_kernel<CT, CS1, TRU, MODE, C4>), dim3(p.B * p.nbpp), dim3(kThreads), 0, st, p);
   return DPFT_OK;
@@ -2022,9 +2610,32 @@ int launch_reduce_t(const IterParams& p, hipStream_t st) {
   return tru ? launch_reduce_k<CT, CS1, true, 0>(p, st) : launch_reduce_k<CT, CS1, false, 0>(p, st);
 }
 
+template <int CT, bool TRU, int MODE>
+int launch_wgmarch(IterParams p, hipStream_t st) {
+  const void* k = reinterpret_cast<const void*>(&ic_wgmarch_kernel<CT, TRU, MODE>);
+  const int cap = resident_blocks(k);
+  if (cap <= 0) return fail(DPFT_E_HIP, "occupancy query failed");
+#ifdef DPFT_GRID_DEN
+  const int capd = cap * DPFT_GRID_NUM / DPFT_GRID_DEN;
+#else
+  const int capd = cap;
+#endif
+  // at least ~4 rows per workgroup (the row pipeline is two rows deep)
+  const int units = p.tiles_x * p.H;
+  p.nbpp = std::max(1, std::min(capd / p.B, units / 4));
+  p.fin.nbpp = p.nbpp;
+  hipLaunchKernelGGL((ic_wgmarch_kernel<CT, TRU, MODE>), dim3(p.B * p.nbpp), dim3(kThreads), 0, st, p);
+  return DPFT_OK;
+}
+
 template <int CT>
 int launch_reduce_c4(const IterParams& p, hipStream_t st) {
   const bool tru = (p.flags & DPFT_REMOVE_TRU_SIGMA) != 0;
+  if constexpr (kWgMarch && CT > 0 && CT % 16 == 0) {
+    if (p.flags & DPFT_NO_UNCERTAINTY) return launch_wgmarch<CT, false, 2>(p, st);
+    if (!(p.flags & DPFT_COMBINE_ICP))
+      return tru ? launch_wgmarch<CT, true, 0>(p, st) : launch_wgmarch<CT, false, 0>(p, st);
+  }
   if (p.flags & DPFT_NO_UNCERTAINTY) return launch_reduce_k<CT, true, false, 2, true>(p, st);
   if (p.flags & DPFT_COMBINE_ICP)
     return tru ? launch_reduce_k<CT, true, true, 1, true>(p, st) : launch_reduce_k<CT, true, false, 1, true>(p, st);
@@ -2034,7 +2645,7 @@ int launch_reduce_c4(const IterParams& p, hipStream_t st) {
 int launch_reduce(const IterParams& p, hipStream_t st) {
   int rc;
   if (p.flags & DPFT_FEATURES_C4) {
-    rc = p.C == 32 ? launch_reduce_c4<32>(p, st) : launch_reduce_c4<0>(p, st);
+    rc = p.C == 32 ? launch_reduce_c4<32>(p, st) : p.C == 16 ? launch_reduce_c4<16>(p, st) : launch_reduce_c4<0>(p, st);
   } else if (p.Cs == 1 || (p.flags & DPFT_NO_UNCERTAINTY)) {
     switch (p.C) {
       case 8: rc = launch_reduce_t<8, true>(p, st); break;
