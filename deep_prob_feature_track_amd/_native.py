@@ -17,6 +17,7 @@ REMOVE_TRU_SIGMA = 0x1
 COMBINE_ICP = 0x2
 NO_UNCERTAINTY = 0x4
 FEATURES_C4 = 0x8
+SCHEDULES = {"auto": 0x00, "march": 0x10, "split": 0x20}  # DPFT_SCHED_*
 STATUS_NONFINITE = 0x1
 ABI_VERSION = 1
 

@@ -98,10 +98,22 @@ constexpr int kRowsPerStep = 4;        // one row per wave per step
 #define DPFT_RING_M 2
 #endif
 constexpr bool kMarch = DPFT_MARCH != 0;  // channel-quad reduce: row-marching window (1) or 4-row tiles (0)
-#ifndef DPFT_WGMARCH
-#define DPFT_WGMARCH 0
+#ifndef DPFT_SPLIT_MAX_PIXELS
+#define DPFT_SPLIT_MAX_PIXELS 40000
 #endif
-constexpr bool kWgMarch = DPFT_WGMARCH != 0;  // channel-quad U_IC / IC: workgroup-marching kernel
+constexpr long kSplitMaxPixels = DPFT_SPLIT_MAX_PIXELS;
+#ifndef DPFT_SPLIT_SEPFIN
+#define DPFT_SPLIT_SEPFIN 1
+#endif
+constexpr bool kSplitSepFin = DPFT_SPLIT_SEPFIN != 0;
+#ifndef DPFT_SEPFIN_MAX_PIXELS
+#define DPFT_SEPFIN_MAX_PIXELS 0
+#endif
+constexpr long kSepFinMaxPixels = DPFT_SEPFIN_MAX_PIXELS;  // ic_reduce_kernel levels finalized by a separate launch  // levels up to this size per pair: ic_split_kernel  // channel-quad U_IC / IC: workgroup-marching kernel
+#ifndef DPFT_MARCH_ROWS
+#define DPFT_MARCH_ROWS 1
+#endif
+constexpr int kMarchRows = DPFT_MARCH_ROWS;  // rows per marching step (1, or 2: -10 % f1 traffic, +11 % VALU, 4 % slower)
 constexpr int kRingM = DPFT_RING_M;       // quads in flight on the marching path (kRingM - 1 ahead)
 #ifndef DPFT_F0_AUX
 #define DPFT_F0_AUX 2
@@ -201,6 +213,11 @@ __device__ bool block_is_last(uint32_t* counter, uint32_t add, uint32_t total) {
   __syncthreads();
   return s_last != 0;
 }
+
+template <int W_>
+struct WaveIdx {  // compile-time index tag (wave, row, buffer parity)
+  static constexpr int value = W_;
+};
 
 __device__ __forceinline__ int wave_id() { return __builtin_amdgcn_readfirstlane(threadIdx.x >> 6); }
 
@@ -776,7 +793,7 @@ __device__ void block_minmax2(float& mn_a, float& mx_a, float& mn_b, float& mx_b
   }
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   __syncthreads();  // sm may still be read by a previous call
-  if (lane == 0) {
+  if (lane == 0 && wave < 4) {  // workgroups wider than kThreads: the extra waves carry no data
     sm[0][wave] = mn_a;
     sm[1][wave] = mx_a;
     sm[2][wave] = mn_b;
@@ -834,6 +851,7 @@ __device__ void pair_reduce(const FinParams& q, int b) {
   const float* rec = q.rec + (size_t)b * q.nbpp * kRec;  // slots of pair b's workgroups
   const int n = q.nbpp;
   double* pr = q.prec + (size_t)b * kPRec;
+  // (workgroups wider than kThreads: threads >= kThreads only take part in the barriers)
   if (tid < 128) {
     double s[21];
 #pragma unroll
@@ -851,7 +869,7 @@ __device__ void pair_reduce(const FinParams& q, int b) {
     if (lane == 0)
 #pragma unroll
       for (int i = 0; i < 21; ++i) shs[wave][i] = s[i];
-  } else {
+  } else if (tid < kThreads) {
     double s[7];
 #pragma unroll
     for (int i = 0; i < 7; ++i) s[i] = 0.0;
@@ -945,29 +963,30 @@ __device__ void pair_reduce(const FinParams& q, int b) {
 // Run by the workgroup that completes the last pair: batch-global truncated-sigma
 // extrema over the pair records, corrections, then one thread per pair solves and
 // updates its pose (algorithms.py:2017-2103).
-__device__ void finalize_batch(const FinParams& q) {
+// `get(b, i)` reads field i of pair b's fp64 record (kPRec layout).
+template <class Get>
+__device__ void finalize_batch_from(const FinParams& q, Get get) {
   const bool tru = (q.flags & DPFT_REMOVE_TRU_SIGMA) != 0;
   const int B = q.B;
   float gmin = INFINITY, gmax = -INFINITY, u0 = INFINITY, u1 = -INFINITY;
   if (tru) {
-    for (int b = threadIdx.x; b < B; b += kThreads) {
-      gmin = fminf(gmin, (float)ld_ag(q.prec + (size_t)b * kPRec + P_MN_ALL));
-      gmax = fmaxf(gmax, (float)ld_ag(q.prec + (size_t)b * kPRec + P_MX_ALL));
+    for (int b = threadIdx.x; threadIdx.x < kThreads && b < B; b += kThreads) {
+      gmin = fminf(gmin, (float)get(b, P_MN_ALL));
+      gmax = fmaxf(gmax, (float)get(b, P_MX_ALL));
     }
     block_minmax2(gmin, gmax, u0, u1);
   }
-  for (int b = threadIdx.x; b < B; b += kThreads) {
-    const double* pr = q.prec + (size_t)b * kPRec;
+  for (int b = threadIdx.x; threadIdx.x < kThreads && b < B; b += kThreads) {
     double sv[28];
 #pragma unroll
-    for (int k = 0; k < 28; ++k) sv[k] = ld_ag(pr + P_S + k);
+    for (int k = 0; k < 28; ++k) sv[k] = get(b, P_S + k);
     if (tru) {
-      if ((float)ld_ag(pr + P_MN0) == gmin)
+      if ((float)get(b, P_MN0) == gmin)
 #pragma unroll
-        for (int k = 0; k < 7; ++k) sv[21 + k] += ld_ag(pr + P_CMN + k);
-      if (gmax != gmin && (float)ld_ag(pr + P_MX0) == gmax)
+        for (int k = 0; k < 7; ++k) sv[21 + k] += get(b, P_CMN + k);
+      if (gmax != gmin && (float)get(b, P_MX0) == gmax)
 #pragma unroll
-        for (int k = 0; k < 7; ++k) sv[21 + k] += ld_ag(pr + P_CMX + k);
+        for (int k = 0; k < 7; ++k) sv[21 + k] += get(b, P_CMX + k);
     }
     bool finite = true;
 #pragma unroll
@@ -990,6 +1009,9 @@ __device__ void finalize_batch(const FinParams& q) {
     if (q.invalid_out) q.invalid_out[b] = (int32_t)sv[27];
     solve_and_update(sv, sv + 21, q.R + 9 * b, q.t + 3 * b);
   }
+}
+__device__ void finalize_batch(const FinParams& q) {
+  finalize_batch_from(q, [&](int b, int i) { return ld_ag(q.prec + (size_t)b * kPRec + i); });
 }
 
 // Last workgroup of a residual launch: loss[b] = sum / (HW - #invalid)
@@ -1286,101 +1308,137 @@ __global__ __launch_bounds__(kThreads, DPFT_MIN_WAVES) void ic_reduce_kernel(Ite
       y = u - strip * H;
       xs = strip * kTileOut - 1 + lane;
     };
-    // window in LDS, per wave [2 slots][NQ quads][64 lanes]: at row step k slot k & 1 holds
-    // row y - dir and slot (k + 1) & 1 row y; the new row y + dir overwrites the first slot
-    // right after this lane has read it (each lane only ever touches its own column, and a
-    // wave's LDS accesses complete in order: no barrier)
+    // window in LDS, per wave [2 slots][NQ quads][64 lanes] (each lane only ever touches
+    // its own column and a wave's LDS accesses complete in order: no barrier)
     f32x4* win = lds_win[wave];
     float sprev = 0.f, scur = 0.f;
     struct QuadM {
       f32x4 f;      // f0 row y + dir
       f32x4 t[4];   // f1 taps (see gather4 / QuadLoadsR)
     };
-    float d_cur[1] = {0.f};
-    if (nrows > 0) {
-      int xs, y;
-      unit_pos(0, xs, y);
-      d_cur[0] = bld(rd0, y * W * 4 + min(max(xs, 0), W - 1) * 4, 0);
-    }
-    for (int k = 0; k < nrows; ++k) {
-      int xs, y;
-      unit_pos(k, xs, y);
-      const float dv[1] = {d_cur[0]};
-      if (k + 1 < nrows) {
-        int xn, yn;
-        unit_pos(k + 1, xn, yn);
-        d_cur[0] = bld(rd0, yn * W * 4 + min(max(xn, 0), W - 1) * 4, 0);
+    // d of the next step's (up to) two rows, prefetched one step ahead
+    float dnx[2] = {0.f, 0.f};
+    auto load_d2 = [&](int k, float (&dd)[2]) {
+#pragma unroll
+      for (int r = 0; r < 2; ++r) {
+        int xs, y;
+        unit_pos(min(k + r, nrows - 1), xs, y);
+        dd[r] = bld(rd0, y * W * 4 + min(max(xs, 0), W - 1) * 4, 0);
       }
+    };
+    if (nrows > 0) load_d2(0, dnx);
+    // One marching step of NS rows (2, or 1 at an odd end / a strip change).  Channel work
+    // goes in units (quad q, row r), rows innermost, so the f1 tap row a pixel of row y
+    // shares with the pixel below it is requested twice back to back (an L1/L2 hit)
+    // instead of one row-step later (after L2 has dropped it: 1.55x f1 traffic).
+    // Window slots: slot 0 = row y - dir, slot 1 = row y; unit (q, 0) reads both and
+    // leaves row y + dir in slot 0, unit (q, 1) reads slot 1 / slot 0 and leaves y + 2 dir
+    // in slot 1, which is the window of the next step.
+    auto stepn = [&](auto NSC, int k) {
+      constexpr int NS = decltype(NSC)::value;
+      constexpr int NU = NQ * NS;
+      int xs, yr[NS];
+      unit_pos(k, xs, yr[0]);
+      if constexpr (NS == 2) {
+        int xs1;
+        unit_pos(k + 1, xs1, yr[1]);
+      }
+      const float dcur[2] = {dnx[0], dnx[1]};
+      if (k + NS < nrows) load_d2(k + NS, dnx);
       const int colq = min(max(xs, 0), W - 1) * 16;
-      if (k == 0 || y == row_restart) {  // prime the window: rows y - dir (replicate-clamped) and y
-        const int yp = min(max(y - dir, 0), H - 1);
+      if (k == 0 || yr[0] == row_restart) {  // prime the window: rows y - dir (replicate-clamped) and y
+        const int yp = min(max(yr[0] - dir, 0), H - 1);
 #pragma unroll
         for (int q = 0; q < NQ; ++q) {
-          win[((k & 1) * NQ + q) * 64 + lane] = llvm_buf_load_f32x4(rf0, colq, q * 4 * (int)planeB + yp * W * 16, kF0Aux);
-          win[(((k + 1) & 1) * NQ + q) * 64 + lane] = llvm_buf_load_f32x4(rf0, colq, q * 4 * (int)planeB + y * W * 16, kF0Aux);
+          win[q * 64 + lane] = llvm_buf_load_f32x4(rf0, colq, q * 4 * (int)planeB + yp * W * 16, kF0Aux);
+          win[(NQ + q) * 64 + lane] = llvm_buf_load_f32x4(rf0, colq, q * 4 * (int)planeB + yr[0] * W * 16, kF0Aux);
         }
         if (CS1 && !NOSIG) {
           sprev = bld(rs0, colq >> 2, yp * W * 4);
-          scur = bld(rs0, colq >> 2, y * W * 4);
+          scur = bld(rs0, colq >> 2, yr[0] * W * 4);
         }
       }
-      const int yn = min(max(y + dir, 0), H - 1);
-      Frame F;
-      make_frame_xy(xs, y, dv, F, false);
-      float snew = 0.f;
-      if (CS1 && !NOSIG) snew = bld(rs0, colq >> 2, yn * W * 4);
+      int yn[NS];
+      Frame F[NS];
+      float snew[NS];
+#pragma unroll
+      for (int r = 0; r < NS; ++r) {
+        yn[r] = min(max(yr[r] + dir, 0), H - 1);
+        const float dv[1] = {dcur[r]};
+        make_frame_xy(xs, yr[r], dv, F[r], false);
+        snew[r] = (CS1 && !NOSIG) ? bld(rs0, colq >> 2, yn[r] * W * 4) : 0.f;
+      }
       QuadM L[kRingM];
-      auto issue = [&](QuadM& Q, int q) {
+      auto issue = [&](QuadM& Qm, int q, auto RC) {
+        constexpr int r = decltype(RC)::value;
 #if DPFT_ABL == 1  // profiling ablation: no channel loop (frame + epilogue only)
         return;
 #endif
         const int po = q * 4 * (int)planeB;
-        Q.f = llvm_buf_load_f32x4(rf0, colq, po + yn * W * 16, kF0Aux);
+        Qm.f = llvm_buf_load_f32x4(rf0, colq, po + yn[r] * W * 16, kF0Aux);
 #if DPFT_ABL == 3  // profiling ablation: no f1 gathers
-        Q.t[0] = Q.t[1] = Q.t[2] = Q.t[3] = Q.f;
+        Qm.t[0] = Qm.t[1] = Qm.t[2] = Qm.t[3] = Qm.f;
 #else
-        Q.t[0] = bld4(rf1, F.tp[0].ob0 * 16, po);
-        Q.t[1] = bld4(rf1, F.tp[0].ob0 * 16 + 16, po);
-        Q.t[2] = bld4(rf1, F.tp[0].ob1 * 16, po);
-        Q.t[3] = bld4(rf1, F.tp[0].ob1 * 16 + 16, po);
+        Qm.t[0] = bld4(rf1, F[r].tp[0].ob0 * 16, po);
+        Qm.t[1] = bld4(rf1, F[r].tp[0].ob0 * 16 + 16, po);
+        Qm.t[2] = bld4(rf1, F[r].tp[0].ob1 * 16, po);
+        Qm.t[3] = bld4(rf1, F[r].tp[0].ob1 * 16 + 16, po);
 #endif
       };
-#pragma unroll
-      for (int q = 0; q + 1 < kRingM; ++q)
-        if (q < NQ) issue(L[q], q);
+      static_assert(kRingM == 2 && NQ % 2 == 0, "two units in flight, whole (quad, row) groups per round");
+      issue(L[0], 0, WaveIdx<0>{});
       if (CS1 && !NOSIG) {
-        F.s0r[0] = up ? snew : sprev;
-        F.s0r[1] = scur;
-        F.s0r[2] = up ? sprev : snew;
-        sprev = scur;
-        scur = snew;
+        // sigma0 rows top / centre / bottom of each row (marching direction folded in)
+        const float s1n = snew[0], s2n = snew[NS - 1];
+        F[0].s0r[0] = up ? s1n : sprev;
+        F[0].s0r[1] = scur;
+        F[0].s0r[2] = up ? sprev : s1n;
+        if constexpr (NS == 2) {
+          F[1].s0r[0] = up ? s2n : scur;
+          F[1].s0r[1] = s1n;
+          F[1].s0r[2] = up ? scur : s2n;
+          sprev = s1n;
+          scur = s2n;
+        } else {
+          sprev = scur;
+          scur = s1n;
+        }
       }
-      PixelTerms T;
-      pixel_terms(F, T);
-      f32x2 Q[9];
+      PixelTerms T[NS];
 #pragma unroll
-      for (int i = 0; i < 9; ++i) Q[i] = f32x2{0.f, 0.f};
-      const PairWeights& w = F.pw[0];
-      static_assert(NQ % kRingM == 0, "quads per ring round");
-      auto quad = [&](int q, const QuadM& cur) {
+      for (int r = 0; r < NS; ++r) pixel_terms(F[r], T[r]);
+      f32x2 Q[NS][9];
+#pragma unroll
+      for (int r = 0; r < NS; ++r)
+#pragma unroll
+        for (int i = 0; i < 9; ++i) Q[r][i] = f32x2{0.f, 0.f};
+      auto unitc = [&](int q, const QuadM& cur, auto RC) {
+        constexpr int r = decltype(RC)::value;
 #if DPFT_ABL == 1
         return;
 #endif
-        f32x4* sp = win + ((k & 1) * NQ + q) * 64 + lane;
-        const f32x4 wp = *sp, wc = win[(((k + 1) & 1) * NQ + q) * 64 + lane];
+        f32x4* s0p = win + q * 64 + lane;         // slot 0
+        f32x4* s1p = win + (NQ + q) * 64 + lane;  // slot 1
+        f32x4 wtop, wmid;  // rows above / at the pixel in marching order
+        if constexpr (r == 0) {
+          wtop = *s0p;
+          wmid = *s1p;
+        } else {
+          wtop = *s1p;
+          wmid = *s0p;
+        }
 #if DPFT_ABL == 2  // profiling ablation: loads only
         {
-          const f32x4 z = wp + wc + cur.f + cur.t[0] + cur.t[1] + cur.t[2] + cur.t[3];
-          Q[0] += f32x2{z.x, z.y};
-          Q[1] += f32x2{z.z, z.w};
-          *sp = cur.f;
-          return;
+          const f32x4 z = wtop + wmid + cur.f + cur.t[0] + cur.t[1] + cur.t[2] + cur.t[3];
+          Q[r][0] += f32x2{z.x, z.y};
+          Q[r][1] += f32x2{z.z, z.w};
         }
-#endif
+#else
+        const PairWeights& w = F[r].pw[0];
 #pragma unroll
         for (int h = 0; h < 2; ++h) {  // channels 4q + 2h, 4q + 2h + 1
           auto half = [&](const f32x4& v) { return h ? f32x2{v.z, v.w} : f32x2{v.x, v.y}; };
-          const f32x2 fp = half(wp), fm = half(wc), fn = half(cur.f);
+          const f32x2 fp = half(wtop), fm = half(wmid), fn = half(cur.f);
           const f32x2 V = (fp + fn) + 2.0f * fm;
           const f32x2 D = (fn - fp) * dirf;  // bottom - top
           const f32x2 x = f32x2{lane_from_right(V.x) - lane_from_left(V.x), lane_from_right(V.y) - lane_from_left(V.y)};
@@ -1391,38 +1449,45 @@ __global__ __launch_bounds__(kThreads, DPFT_MIN_WAVES) void ic_reduce_kernel(Ite
           const f32x2 gx = x * inv, gy = yv * inv;
           const f32x2 res = (half(cur.t[0]) * w.w0 + half(cur.t[1]) * w.w1 + half(cur.t[2]) * w.w2 +
                              half(cur.t[3]) * w.w3) - fm;
-          Q[0] += gx * gx;
-          Q[1] += gx * gy;
-          Q[2] += gy * gy;
-          Q[3] += gx * res;
-          Q[4] += gy * res;
-          Q[5] += res * res;
-          Q[6] += gx;
-          Q[7] += gy;
-          Q[8] += res;
+          Q[r][0] += gx * gx;
+          Q[r][1] += gx * gy;
+          Q[r][2] += gy * gy;
+          Q[r][3] += gx * res;
+          Q[r][4] += gy * res;
+          Q[r][5] += res * res;
+          Q[r][6] += gx;
+          Q[r][7] += gy;
+          Q[r][8] += res;
         }
-        *sp = cur.f;
+#endif
+        if constexpr (NS == 1) {  // window (y, y + dir)
+          *s0p = wmid;
+          *s1p = cur.f;
+        } else if constexpr (r == 0) {
+          *s0p = cur.f;
+        } else {
+          *s1p = cur.f;
+        }
       };
       // every ring round but the last refills unconditionally: each load set keeps its registers
+      constexpr int r1 = 1 % NS;  // row of the odd units
 #pragma unroll 1
-      for (int q0 = 0; q0 < NQ - kRingM; q0 += kRingM) {
-#pragma unroll
-        for (int qq = 0; qq < kRingM; ++qq) {
-          issue(L[(qq + kRingM - 1) % kRingM], q0 + qq + kRingM - 1);
-          quad(q0 + qq, L[qq]);
-        }
+      for (int u0 = 0; u0 < NU - 2; u0 += 2) {
+        issue(L[1], (u0 + 1) / NS, WaveIdx<r1>{});
+        unitc(u0 / NS, L[0], WaveIdx<0>{});
+        issue(L[0], (u0 + 2) / NS, WaveIdx<0>{});
+        unitc((u0 + 1) / NS, L[1], WaveIdx<r1>{});
       }
+      issue(L[1], (NU - 1) / NS, WaveIdx<r1>{});
+      unitc((NU - 2) / NS, L[0], WaveIdx<0>{});
+      unitc((NU - 1) / NS, L[1], WaveIdx<r1>{});
 #pragma unroll
-      for (int qq = 0; qq < kRingM; ++qq) {
-        if (qq == 0) issue(L[kRingM - 1], NQ - 1);
-        quad(NQ - kRingM + qq, L[qq]);
-      }
-      Sums S;
-      {
+      for (int r = 0; r < NS; ++r) {
+        Sums S;
         float q[9];
 #pragma unroll
-        for (int i = 0; i < 9; ++i) q[i] = Q[i].x + Q[i].y;
-        const float A = T.inv_s[0], bx = T.kk[0] * T.hx[0], by = T.kk[0] * T.hy[0], A2 = A * A;
+        for (int i = 0; i < 9; ++i) q[i] = Q[r][i].x + Q[r][i].y;
+        const float A = T[r].inv_s[0], bx = T[r].kk[0] * T[r].hx[0], by = T[r].kk[0] * T[r].hy[0], A2 = A * A;
         S.Saa[0] = A2 * q[0] + 2.0f * A * bx * q[3] + bx * bx * q[5];
         S.Sab[0] = A2 * q[1] + A * by * q[3] + A * bx * q[4] + bx * by * q[5];
         S.Sbb[0] = A2 * q[2] + 2.0f * A * by * q[4] + by * by * q[5];
@@ -1430,8 +1495,24 @@ __global__ __launch_bounds__(kThreads, DPFT_MIN_WAVES) void ic_reduce_kernel(Ite
         S.Sb[0] = A * q[7] + by * q[8];
         S.Sar[0] = A2 * q[3] + A * bx * q[5];
         S.Sbr[0] = A2 * q[4] + A * by * q[5];
+        finish_pixels(F[r], T[r], S);
       }
-      finish_pixels(F, T, S);
+    };
+    for (int k = 0; k < nrows;) {
+      // two rows per step unless only one is left or the second starts a new strip
+      bool two = kMarchRows == 2 && k + 1 < nrows;
+      if (two) {
+        int xs1, y1;
+        unit_pos(k + 1, xs1, y1);
+        two = y1 != row_restart;
+      }
+      if (two) {
+        stepn(WaveIdx<2>{}, k);
+        k += 2;
+      } else {
+        stepn(WaveIdx<1>{}, k);
+        k += 1;
+      }
     }
   } else if constexpr (C4) {
     // ---- channel-quad layout: the per-pixel weights factor out of the channel sums
@@ -1719,60 +1800,183 @@ __global__ __launch_bounds__(kThreads, DPFT_MIN_WAVES) void ic_reduce_kernel(Ite
   }
 }
 
-// ============================================================ workgroup-marching reduce kernel
-// Channel-quad layout, one sigma plane, U_IC (MODE 0) or IC (MODE 2), C % 16 == 0.
-// A WORKGROUP owns a contiguous run of (column strip, row) units of its pair and
-// marches it row by row; its 4 waves split the channel quads of every row (wave w:
-// quads w*QW .. w*QW+QW-1), so one workgroup-row moves all channels in a quarter of
-// the time a single wave needs and only ~2 workgroups per CU are in flight: the f1
-// tap rows a row shares with the next one are still in L2 when the next row asks
-// (each f1 row comes from HBM ~once; the per-wave march re-fetched it, 1.55x), and f0
-// comes from HBM once through a per-wave register window of rows y - dir, y.
-// Per row only ONE wave computes the warp / taps / occlusion / sigma terms (the wave
-// ((m - 2) & 3) for row m, two rows ahead) and publishes them in LDS; the channel
-// loads of row m + 1 are issued before row m is computed (two row buffers), and the
-// four waves' channel sums meet in LDS behind one barrier per row.  Every wave then
-// forms the per-pixel sums S and accumulates its own share of the 27 normal-equation
-// entries (wave 3: JtR, invalid count and the truncated-sigma extrema).
-template <int W_>
-struct WaveIdx {
-  static constexpr int value = W_;
+// ============================================================ split normal-equation accumulation
+// Kernels whose 4 waves cooperate on the same pixels (each wave a share of the channel
+// quads) meet in LDS with the per-pixel channel sums; then every wave accumulates a
+// quarter of the 27 normal-equation entries of the same pixels: wave w < 3 the JtJ
+// upper-triangle entries 7w .. 7w + 6 (row-major), wave 3 the six JtR entries, the
+// invalid count and the truncated-sigma extremum bookkeeping (finish_pixels' logic).
+template <bool TRU, bool NOSIG, int NW = 4>
+struct SplitAcc {
+  static constexpr float kFill = NOSIG ? 1e-3f : 1e-6f;  // weighted residual of invalid pixels
+  static constexpr int EPW = (21 + NW - 2) / (NW - 1);   // JtJ entries per wave (waves 0 .. NW-2)
+  static constexpr int NA = EPW > 7 ? EPW : 7;           // the last wave: 6 JtR + invalid count
+  float accw[NA];
+  float mn_all, mn0, mx_all, mx0;
+
+  __device__ __forceinline__ void init(int wave, int lane, float (*lds_ext)[64]) {
+#pragma unroll
+    for (int i = 0; i < NA; ++i) accw[i] = 0.0f;
+    mn_all = mn0 = INFINITY;
+    mx_all = mx0 = -INFINITY;
+    if (TRU && wave == NW - 1) {
+#pragma unroll
+      for (int i = 0; i < 14; ++i) lds_ext[i][lane] = 0.0f;
+    }
+  }
+
+  // Sa, Sb, Sar, Sbr already negated (the linear terms of J_c = -(a_c Jx + b_c Jy))
+  template <int w>
+  __device__ __forceinline__ void add_w(int lane, float Saa, float Sab, float Sbb, float Sa, float Sb, float Sar,
+                                        float Sbr, const float* Jx, const float* Jy, bool invalid, float sr,
+                                        float (*lds_ext)[64]) {
+    if constexpr (w < NW - 1) {
+      int kq = 0;
+#pragma unroll
+      for (int i = 0; i < 6; ++i) {
+        const float Pi = Saa * Jx[i] + Sab * Jy[i], Qi = Sab * Jx[i] + Sbb * Jy[i];
+#pragma unroll
+        for (int j = i; j < 6; ++j) {
+          if (kq >= EPW * w && kq < EPW * w + EPW) accw[kq - EPW * w] += Pi * Jx[j] + Qi * Jy[j];
+          ++kq;
+        }
+      }
+    } else {
+      const float cA = invalid ? kFill * Sa : Sar;
+      const float cB = invalid ? kFill * Sb : Sbr;
+#pragma unroll
+      for (int i = 0; i < 6; ++i) accw[i] -= cA * Jx[i] + cB * Jy[i];
+      accw[6] += invalid ? 1.0f : 0.0f;
+      if (TRU) {
+        mn_all = fminf(mn_all, sr);
+        mx_all = fmaxf(mx_all, sr);
+        const bool le = sr <= mn0, ge = sr >= mx0;
+        if (le || ge) {
+          float corr[7];
+          const float dA = invalid ? 0.0f : (1e-6f * Sa - Sar);
+          const float dB = invalid ? 0.0f : (1e-6f * Sb - Sbr);
+#pragma unroll
+          for (int i = 0; i < 6; ++i) corr[i] = -(dA * Jx[i] + dB * Jy[i]);
+          corr[6] = invalid ? 0.0f : 1.0f;
+          if (le) {
+            const bool reset = sr < mn0;
+            mn0 = sr;
+#pragma unroll
+            for (int i = 0; i < 7; ++i) lds_ext[i][lane] = (reset ? 0.0f : lds_ext[i][lane]) + corr[i];
+          }
+          if (ge) {
+            const bool reset = sr > mx0;
+            mx0 = sr;
+#pragma unroll
+            for (int i = 0; i < 7; ++i) lds_ext[7 + i][lane] = (reset ? 0.0f : lds_ext[7 + i][lane]) + corr[i];
+          }
+        }
+      }
+    }
+  }
+  template <int w = 0>
+  __device__ __forceinline__ void add(int wave, int lane, float Saa, float Sab, float Sbb, float Sa, float Sb,
+                                      float Sar, float Sbr, const float* Jx, const float* Jy, bool invalid, float sr,
+                                      float (*lds_ext)[64]) {
+    if (wave == w || w == NW - 1) {
+      add_w<w>(lane, Saa, Sab, Sbb, Sa, Sb, Sar, Sbr, Jx, Jy, invalid, sr, lds_ext);
+    } else if constexpr (w + 1 < NW) {
+      add<w + 1>(wave, lane, Saa, Sab, Sbb, Sa, Sb, Sar, Sbr, Jx, Jy, invalid, sr, lds_ext);
+    }
+  }
+
+  // Workgroup record: wave w < NW-1 holds JtJ entries EPW w .. EPW w + EPW - 1, the last
+  // wave JtR, the invalid count and the truncated-sigma extrema.
+  __device__ __forceinline__ void write_record(int wave, int lane, float (*lds_ext)[64], float* red, float* out) {
+#pragma unroll
+    for (int i = 0; i < NA; ++i) {
+#pragma unroll
+      for (int off = 32; off > 0; off >>= 1) accw[i] += __shfl_xor(accw[i], off);
+    }
+    if (lane == 0) {
+      if (wave < NW - 1) {
+#pragma unroll
+        for (int i = 0; i < EPW; ++i)
+          if (EPW * wave + i < 21) red[EPW * wave + i] = accw[i];
+      } else {
+#pragma unroll
+        for (int i = 0; i < 7; ++i) red[21 + i] = accw[i];
+      }
+    }
+    if (TRU && wave == NW - 1) {
+      Extremum emn, emx;
+      emn.all = mn_all;
+      emn.v0 = mn0;
+      emx.all = mx_all;
+      emx.v0 = mx0;
+#pragma unroll
+      for (int i = 0; i < 6; ++i) {
+        emn.c[i] = lds_ext[i][lane];
+        emx.c[i] = lds_ext[7 + i][lane];
+      }
+      emn.n = lds_ext[6][lane];
+      emx.n = lds_ext[13][lane];
+      ext_wave_reduce<true>(emn);
+      ext_wave_reduce<false>(emx);
+      if (lane == 0) {
+        red[R_MN_ALL] = emn.all;
+        red[R_MN0] = emn.v0;
+        red[R_NMN] = emn.n;
+        red[R_MX_ALL] = emx.all;
+        red[R_MX0] = emx.v0;
+        red[R_NMX] = emx.n;
+#pragma unroll
+        for (int i = 0; i < 6; ++i) {
+          red[R_CMN + i] = emn.c[i];
+          red[R_CMX + i] = emx.c[i];
+        }
+      }
+    }
+    __syncthreads();
+    const int tid = threadIdx.x;
+    if (tid < (TRU ? R_NMX + 1 : R_NINV + 1)) st_ag(out + tid, red[tid]);
+  }
 };
 
+// Stand-alone finalize (one workgroup per pair): pair records, then the batch solve.
+__global__ __launch_bounds__(kThreads) void finalize_kernel(FinParams q) {
+  pair_reduce(q, blockIdx.x);
+  if (block_is_last(q.done_cnt, 1u, (uint32_t)q.B)) finalize_batch(q);
+}
+
+// ============================================================ channel-split reduce kernel (coarse levels)
+// Channel-quad layout, one sigma plane, U_IC (MODE 0) or IC (MODE 2), C % 16 == 0.
+// For the small pyramid levels, where a wave that walks all channels of a row is a
+// chain of ~10 dependent memory latencies and the device is far from full: one
+// workgroup per (column strip, row) unit (grid-stride over a pair's units), its 4
+// waves split the channel quads, and every wave issues ALL of its loads for the unit
+// at once (f0 rows y-1, y, y+1 and the f1 taps of each of its quads).  The warp /
+// taps / sigma terms are recomputed by each wave (cheap next to the latency they
+// save); the per-pixel channel sums meet in LDS behind one barrier per unit and
+// each wave accumulates its share of the normal equations (SplitAcc).
 template <int CT, bool TRU, int MODE>
-__global__ __launch_bounds__(kThreads, 2) void ic_wgmarch_kernel(IterParams p) {
+__global__ __launch_bounds__(kThreads) void ic_split_kernel(IterParams p) {
   constexpr bool NOSIG = MODE == 2;
   static_assert(MODE != 1, "combine_ICP runs on ic_reduce_kernel");
   constexpr int NQ = CT / 4, QW = NQ / 4;
   static_assert(CT % 16 == 0 && QW >= 1, "4 waves x whole channel quads");
-  constexpr float kFill = NOSIG ? 1e-3f : 1e-6f;
-  // frame slot fields (per lane): tap pair bases, pair weights, inverse depth, pixel terms
-  enum { F_OB0, F_OB1, F_W0, F_W1, F_W2, F_W3, F_D, F_A, F_BX, F_BY, F_INV, F_SR0, kSlotF };
-  __shared__ float fr[4][kSlotF][64];
   __shared__ float qs[2][4][9][64];
   __shared__ float lds_ext[TRU ? 14 : 1][64];
   __shared__ float red[kRec];
 
   const int lane = threadIdx.x & 63, wave = wave_id();
-  const int W = p.W, H = p.H;
+  const int W = p.W, H = p.H, HW = H * W;
   const int kb = xcd_remap(blockIdx.x, gridDim.x);
   const int b = kb / p.nbpp, jb = kb - b * p.nbpp;
   const int U = p.tiles_x * H;
-  const int ubeg = (int)(((long)U * jb) / p.nbpp), uend = (int)(((long)U * (jb + 1)) / p.nbpp);
-  const bool up = (jb & 1) != 0;  // odd workgroups march upwards: shared band boundaries meet in time
-  const int dir = up ? -1 : 1;
-  const float dirf = up ? -1.0f : 1.0f;
   const float g0min = TRU ? dec_ord(p.ext[0]) : 0.f, g0max = TRU ? dec_ord(p.ext[1]) : 0.f;
-  const uint32_t planeB = (uint32_t)(H * W) * 4u;
-  const int HW = H * W;
-
+  const uint32_t planeB = (uint32_t)HW * 4u;
   const float fx = p.K[4 * b + 0], fy = p.K[4 * b + 1], cx = p.K[4 * b + 2], cy = p.K[4 * b + 3];
   float Rm[9], tv[3];
 #pragma unroll
   for (int k = 0; k < 9; ++k) Rm[k] = p.R[9 * b + k];
 #pragma unroll
   for (int k = 0; k < 3; ++k) tv[k] = p.t[3 * b + k];
-
   const auto rf0 = rsrc(p.f0 + (size_t)b * CT * HW, planeB * CT);
   const auto rf1 = rsrc(p.f1 + (size_t)b * CT * HW, planeB * CT);
   const auto rs0 = rsrc(NOSIG ? p.invD0 : p.s0 + (size_t)b * HW, planeB);
@@ -1782,300 +1986,129 @@ __global__ __launch_bounds__(kThreads, 2) void ic_wgmarch_kernel(IterParams p) {
   const uint8_t* m0b = p.mask0 ? p.mask0 + (size_t)b * HW : nullptr;
   const uint8_t* m1b = p.mask1 ? p.mask1 + (size_t)b * HW : nullptr;
 
-  float accw[7];
-#pragma unroll
-  for (int i = 0; i < 7; ++i) accw[i] = 0.0f;
-  float mn_all = INFINITY, mn0 = INFINITY, mx_all = -INFINITY, mx0 = -INFINITY;
-  if (TRU && wave == 3) {
-#pragma unroll
-    for (int i = 0; i < 14; ++i) lds_ext[i][lane] = 0.0f;
-  }
+  SplitAcc<TRU, NOSIG> acc;
+  acc.init(wave, lane, lds_ext);
 
-  struct RowLoads {
-    f32x4 f[QW];     // f0 row y + dir of this wave's quads
-    f32x4 t[QW][4];  // f1 taps (pair bases, see gather4)
-  };
-  RowLoads L[2];
-  f32x4 wprev[QW], wcur[QW];
-
-  // segments: the unit range split at strip boundaries, walked in marching order
-  const int s_first = ubeg / H, s_last = (uend - 1) / H;
-  for (int si = 0; si <= s_last - s_first; ++si) {
-    const int strip = up ? s_last - si : s_first + si;
-    const int ya = max(ubeg - strip * H, 0), yb = min(uend - strip * H, H);
-    const int n = yb - ya;
-    if (n <= 0) continue;
-    __syncthreads();  // the previous segment's last row may still be reading frame slot 0
-    auto yrow = [&](int m) { return up ? yb - 1 - m : ya + m; };
+  auto unit_xy = [&](int u, int& xc, int& y, bool& out_lane) {
+    const int strip = u / H;
+    y = u - strip * H;
     const int xs = strip * kTileOut - 1 + lane;
-    const int xc = min(max(xs, 0), W - 1);
-    const bool out_lane = (lane >= 1) && (lane <= kTileOut) && (xs < W);
-    const int colq = xc * 16;
-
-    // frame-wave state: wave w frames rows m = w + 2 (mod 4), two steps ahead
-    float dpre = 0.f;
-    {
-      const int mf = (wave + 2) & 3;
-      if (mf < n) dpre = bld(rd0, yrow(mf) * W * 4 + xc * 4, 0);
-    }
-    // one pipeline step: row k + 2 framed, row k + 1 loaded, row k reduced.  P = k & 1 is a
-    // template constant so the two row buffers stay in registers (a runtime index would
-    // put them in scratch).
-    auto step = [&](int k, auto PC) {
-      constexpr int P = decltype(PC)::value;
-      const bool framer = ((k & 3) == wave) && (k + 2 < n);
-      // ---- P1: warp / taps of row k + 2, its gathers (issued before this step's channel loads)
-      Warp fw;
-      PairWeights fpw;
-      Gather4 gd1, gs1;
-      float s0t = 0.f, s0m = 0.f, s0b = 0.f, fm1 = 1.0f;
-      bool fm0 = true;
-      if (framer) {
-        const int m = k + 2, y = yrow(m);
-        const float d = dpre;
-        fw = warp_point(xc, y, d, Rm, tv, fx, fy, cx, cy);
-        const Taps tp = make_taps(fw.u, fw.v, H, W);
-        fpw = pair_weights(tp);
-        gd1 = gather4(rd1, tp, 0);
-        if (!NOSIG) {
-          gs1 = gather4(rs1, tp, 0);
-          s0t = bld(rs0, xc * 4, max(y - 1, 0) * W * 4);
-          s0m = bld(rs0, xc * 4, y * W * 4);
-          s0b = bld(rs0, xc * 4, min(y + 1, H - 1) * W * 4);
-        }
-        if (m0b) fm0 = m0b[y * W + xc] != 0;
-        if (m1b) fm1 = bil_u8(m1b, tp);
-        if (m + 4 < n) dpre = bld(rd0, yrow(m + 4) * W * 4 + xc * 4, 0);
-        float* s = &fr[m & 3][0][lane];
-        s[F_OB0 * 64] = __int_as_float(tp.ob0);
-        s[F_OB1 * 64] = __int_as_float(tp.ob1);
-        s[F_W0 * 64] = fpw.w0;
-        s[F_W1 * 64] = fpw.w1;
-        s[F_W2 * 64] = fpw.w2;
-        s[F_W3 * 64] = fpw.w3;
-        s[F_D * 64] = d;
-      }
-      // ---- P2: channel loads of row k + 1 (this wave's quads), window prime at the segment start
-      if (k + 1 >= 0 && k + 1 < n) {
-        const int m = k + 1, y = yrow(m);
-        const int ob0 = __float_as_int(fr[m & 3][F_OB0][lane]), ob1 = __float_as_int(fr[m & 3][F_OB1][lane]);
-        if (m == 0) {
-          const int yp = min(max(y - dir, 0), H - 1);
-#pragma unroll
-          for (int qq = 0; qq < QW; ++qq) {
-            const int po = (wave * QW + qq) * 4 * (int)planeB;
-            wprev[qq] = llvm_buf_load_f32x4(rf0, colq, po + yp * W * 16, kF0Aux);
-            wcur[qq] = llvm_buf_load_f32x4(rf0, colq, po + y * W * 16, kF0Aux);
-          }
-        }
-        const int yn = min(max(y + dir, 0), H - 1);
-        RowLoads& Ld = L[1 - P];
-#pragma unroll
-        for (int qq = 0; qq < QW; ++qq) {
-          const int po = (wave * QW + qq) * 4 * (int)planeB;
-          Ld.f[qq] = llvm_buf_load_f32x4(rf0, colq, po + yn * W * 16, kF0Aux);
-          Ld.t[qq][0] = bld4(rf1, ob0 * 16, po);
-          Ld.t[qq][1] = bld4(rf1, ob0 * 16 + 16, po);
-          Ld.t[qq][2] = bld4(rf1, ob1 * 16, po);
-          Ld.t[qq][3] = bld4(rf1, ob1 * 16 + 16, po);
-        }
-      }
-      // ---- P3: channel sums of row k over this wave's quads -> LDS
-      if (k >= 0) {
-        const RowLoads& Ld = L[P];
-        const float w0 = fr[k & 3][F_W0][lane], w1 = fr[k & 3][F_W1][lane], w2 = fr[k & 3][F_W2][lane],
-                    w3 = fr[k & 3][F_W3][lane];
-        f32x2 Q[9];
-#pragma unroll
-        for (int i = 0; i < 9; ++i) Q[i] = f32x2{0.f, 0.f};
-#pragma unroll
-        for (int qq = 0; qq < QW; ++qq) {
-#pragma unroll
-          for (int h = 0; h < 2; ++h) {
-            auto half = [&](const f32x4& v) { return h ? f32x2{v.z, v.w} : f32x2{v.x, v.y}; };
-            const f32x2 fp = half(wprev[qq]), fm = half(wcur[qq]), fn = half(Ld.f[qq]);
-            const f32x2 V = (fp + fn) + 2.0f * fm;
-            const f32x2 D = (fn - fp) * dirf;  // bottom - top
-            const f32x2 x = f32x2{lane_from_right(V.x) - lane_from_left(V.x), lane_from_right(V.y) - lane_from_left(V.y)};
-            const f32x2 yv =
-                f32x2{lane_from_left(D.x) + lane_from_right(D.x), lane_from_left(D.y) + lane_from_right(D.y)} + 2.0f * D;
-            const f32x2 n2 = x * x + yv * yv + 1e-8f;
-            const f32x2 inv = f32x2{__builtin_amdgcn_rsqf(n2.x), __builtin_amdgcn_rsqf(n2.y)};
-            const f32x2 gx = x * inv, gy = yv * inv;
-            const f32x2 res =
-                (half(Ld.t[qq][0]) * w0 + half(Ld.t[qq][1]) * w1 + half(Ld.t[qq][2]) * w2 + half(Ld.t[qq][3]) * w3) - fm;
-            Q[0] += gx * gx;
-            Q[1] += gx * gy;
-            Q[2] += gy * gy;
-            Q[3] += gx * res;
-            Q[4] += gy * res;
-            Q[5] += res * res;
-            Q[6] += gx;
-            Q[7] += gy;
-            Q[8] += res;
-          }
-          wprev[qq] = wcur[qq];
-          wcur[qq] = Ld.f[qq];
-        }
-#pragma unroll
-        for (int i = 0; i < 9; ++i) qs[P][wave][i][lane] = Q[i].x + Q[i].y;
-      }
-      // ---- P5: occlusion / mask / sigma terms of row k + 2 (its gathers are older than
-      // this step's channel loads: no extra wait)
-      if (framer) {
-        const int m = k + 2;
-        const float d1w = bilp(gd1, fpw);
-        const bool ok = (fw.iz > d1w - 0.1f) && (fw.u > 0.0f) && (fw.u < (float)W) && (fw.v > 0.0f) &&
-                        (fw.v < (float)H);
-        bool invalid = !ok || !out_lane || !fm0 || !(fm1 > 0.0f);
-        float A = 1.0f, bx = 0.0f, by = 0.0f, sr0 = 0.0f;
-        if (!NOSIG) {
-          float hx, hy;
-          sobel_cols(s0t, s0m, s0b, hx, hy);
-          sr0 = bilp(gs1, fpw);
-          const float sg = sqrtf(sr0 * sr0 + s0m * s0m);
-          A = __builtin_amdgcn_rcpf(sg);
-          const float kk = s0m * (A * A * A);
-          bx = kk * hx;
-          by = kk * hy;
-          if (TRU) invalid = invalid || (s0m == g0min) || (s0m == g0max);
-        }
-        float* s = &fr[m & 3][0][lane];
-        s[F_A * 64] = A;
-        s[F_BX * 64] = bx;
-        s[F_BY * 64] = by;
-        s[F_INV * 64] = invalid ? 1.0f : 0.0f;
-        s[F_SR0 * 64] = sr0;
-      }
-      __syncthreads();
-      // ---- P7: per-pixel sums and this wave's share of the normal equations of row k
-      if (k >= 0 && out_lane) {
-        float q[9];
-#pragma unroll
-        for (int i = 0; i < 9; ++i)
-          q[i] = ((qs[P][0][i][lane] + qs[P][1][i][lane]) + qs[P][2][i][lane]) + qs[P][3][i][lane];
-        const float* s = &fr[k & 3][0][lane];
-        const float A = s[F_A * 64], bx = s[F_BX * 64], by = s[F_BY * 64], d = s[F_D * 64];
-        const bool invalid = s[F_INV * 64] != 0.0f;
-        const float A2 = A * A;
-        const float Saa = A2 * q[0] + 2.0f * A * bx * q[3] + bx * bx * q[5];
-        const float Sab = A2 * q[1] + A * by * q[3] + A * bx * q[4] + bx * by * q[5];
-        const float Sbb = A2 * q[2] + 2.0f * A * by * q[4] + by * by * q[5];
-        const float Sa = -(A * q[6] + bx * q[8]), Sb = -(A * q[7] + by * q[8]);
-        const float Sar = -(A2 * q[3] + A * bx * q[5]), Sbr = -(A2 * q[4] + A * by * q[5]);
-        float xr, yr;
-        {
-#pragma clang fp contract(off)
-          xr = ((float)xc - cx) / fx;
-          yr = ((float)yrow(k) - cy) / fy;
-        }
-        float Jx[6], Jy[6];
-        warp_jac(xr, yr, d, fx, fy, Jx, Jy);
-        auto share = [&](auto WV) {
-          constexpr int w = decltype(WV)::value;
-          if constexpr (w < 3) {  // JtJ entries 7w .. 7w + 6 (upper triangle, row-major)
-            int kq = 0;
-#pragma unroll
-            for (int i = 0; i < 6; ++i) {
-              const float Pi = Saa * Jx[i] + Sab * Jy[i], Qi = Sab * Jx[i] + Sbb * Jy[i];
-#pragma unroll
-              for (int j = i; j < 6; ++j) {
-                if (kq >= 7 * w && kq < 7 * w + 7) accw[kq - 7 * w] += Pi * Jx[j] + Qi * Jy[j];
-                ++kq;
-              }
-            }
-          } else {  // JtR (weighted residual of invalid pixels = kFill on every channel), invalid count
-            const float cA = invalid ? kFill * Sa : Sar;
-            const float cB = invalid ? kFill * Sb : Sbr;
-#pragma unroll
-            for (int i = 0; i < 6; ++i) accw[i] -= cA * Jx[i] + cB * Jy[i];
-            accw[6] += invalid ? 1.0f : 0.0f;
-            if (TRU) {
-              const float sr = s[F_SR0 * 64];
-              mn_all = fminf(mn_all, sr);
-              mx_all = fmaxf(mx_all, sr);
-              const bool le = sr <= mn0, ge = sr >= mx0;
-              if (le || ge) {
-                float corr[7];
-                const float dA = invalid ? 0.0f : (1e-6f * Sa - Sar);
-                const float dB = invalid ? 0.0f : (1e-6f * Sb - Sbr);
-#pragma unroll
-                for (int i = 0; i < 6; ++i) corr[i] = -(dA * Jx[i] + dB * Jy[i]);
-                corr[6] = invalid ? 0.0f : 1.0f;
-                if (le) {
-                  const bool reset = sr < mn0;
-                  mn0 = sr;
-#pragma unroll
-                  for (int i = 0; i < 7; ++i) lds_ext[i][lane] = (reset ? 0.0f : lds_ext[i][lane]) + corr[i];
-                }
-                if (ge) {
-                  const bool reset = sr > mx0;
-                  mx0 = sr;
-#pragma unroll
-                  for (int i = 0; i < 7; ++i)
-                    lds_ext[7 + i][lane] = (reset ? 0.0f : lds_ext[7 + i][lane]) + corr[i];
-                }
-              }
-            }
-          }
-        };
-        switch (wave) {
-          case 0: share(WaveIdx<0>{}); break;
-          case 1: share(WaveIdx<1>{}); break;
-          case 2: share(WaveIdx<2>{}); break;
-          default: share(WaveIdx<3>{}); break;
-        }
-      }
-    };
-    for (int k = -2; k < n; k += 2) {
-      step(k, WaveIdx<0>{});
-      if (k + 1 < n) step(k + 1, WaveIdx<1>{});
-    }
+    xc = min(max(xs, 0), W - 1);
+    out_lane = (lane >= 1) && (lane <= kTileOut) && (xs < W);
+  };
+  float dnext = 0.f;
+  if (jb < U) {
+    int xc, y;
+    bool ol;
+    unit_xy(jb, xc, y, ol);
+    dnext = bld(rd0, y * W * 4 + xc * 4, 0);
   }
-
-  // ---- workgroup record: wave w holds entries 7w .. 7w + 6 (wave 3: JtR + invalid count)
-#pragma unroll
-  for (int i = 0; i < 7; ++i) {
-#pragma unroll
-    for (int off = 32; off > 0; off >>= 1) accw[i] += __shfl_xor(accw[i], off);
-  }
-  if (lane == 0) {
-#pragma unroll
-    for (int i = 0; i < 7; ++i) red[7 * wave + i] = accw[i];
-  }
-  if (TRU && wave == 3) {
-    Extremum emn, emx;
-    emn.all = mn_all;
-    emn.v0 = mn0;
-    emx.all = mx_all;
-    emx.v0 = mx0;
-#pragma unroll
-    for (int i = 0; i < 6; ++i) {
-      emn.c[i] = lds_ext[i][lane];
-      emx.c[i] = lds_ext[7 + i][lane];
+  int par = 0;
+  for (int u = jb; u < U; u += p.nbpp, par ^= 1) {
+    int xc, y;
+    bool out_lane;
+    unit_xy(u, xc, y, out_lane);
+    const float d = dnext;
+    if (u + p.nbpp < U) {
+      int xn, yn;
+      bool oln;
+      unit_xy(u + p.nbpp, xn, yn, oln);
+      dnext = bld(rd0, yn * W * 4 + xn * 4, 0);
     }
-    emn.n = lds_ext[6][lane];
-    emx.n = lds_ext[13][lane];
-    ext_wave_reduce<true>(emn);
-    ext_wave_reduce<false>(emx);
-    if (lane == 0) {
-      red[R_MN_ALL] = emn.all;
-      red[R_MN0] = emn.v0;
-      red[R_NMN] = emn.n;
-      red[R_MX_ALL] = emx.all;
-      red[R_MX0] = emx.v0;
-      red[R_NMX] = emx.n;
+    const Warp fw = warp_point(xc, y, d, Rm, tv, fx, fy, cx, cy);
+    const Taps tp = make_taps(fw.u, fw.v, H, W);
+    const PairWeights pw = pair_weights(tp);
+    const Gather4 gd1 = gather4(rd1, tp, 0);
+    Gather4 gs1{0.f, 0.f, 0.f, 0.f};
+    float s0t = 0.f, s0m = 0.f, s0b = 0.f;
+    const int yt = max(y - 1, 0), yb = min(y + 1, H - 1);
+    if (!NOSIG) {
+      gs1 = gather4(rs1, tp, 0);
+      s0t = bld(rs0, xc * 4, yt * W * 4);
+      s0m = bld(rs0, xc * 4, y * W * 4);
+      s0b = bld(rs0, xc * 4, yb * W * 4);
+    }
+    f32x4 ft[QW], fm[QW], fb[QW], t[QW][4];
 #pragma unroll
-      for (int i = 0; i < 6; ++i) {
-        red[R_CMN + i] = emn.c[i];
-        red[R_CMX + i] = emx.c[i];
+    for (int qq = 0; qq < QW; ++qq) {
+      const int po = (wave * QW + qq) * 4 * (int)planeB;
+      ft[qq] = bld4(rf0, xc * 16, po + yt * W * 16);
+      fm[qq] = bld4(rf0, xc * 16, po + y * W * 16);
+      fb[qq] = bld4(rf0, xc * 16, po + yb * W * 16);
+      t[qq][0] = bld4(rf1, tp.ob0 * 16, po);
+      t[qq][1] = bld4(rf1, tp.ob0 * 16 + 16, po);
+      t[qq][2] = bld4(rf1, tp.ob1 * 16, po);
+      t[qq][3] = bld4(rf1, tp.ob1 * 16 + 16, po);
+    }
+    const bool fm0 = m0b ? (m0b[y * W + xc] != 0) : true;
+    const float fm1 = m1b ? bil_u8(m1b, tp) : 1.0f;
+    // channel sums of this wave's quads
+    f32x2 Q[9];
+#pragma unroll
+    for (int i = 0; i < 9; ++i) Q[i] = f32x2{0.f, 0.f};
+#pragma unroll
+    for (int qq = 0; qq < QW; ++qq) {
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        auto half = [&](const f32x4& v) { return h ? f32x2{v.z, v.w} : f32x2{v.x, v.y}; };
+        const f32x2 a = half(ft[qq]), c = half(fm[qq]), e = half(fb[qq]);
+        const f32x2 V = (a + e) + 2.0f * c;
+        const f32x2 D = e - a;
+        const f32x2 x = f32x2{lane_from_right(V.x) - lane_from_left(V.x), lane_from_right(V.y) - lane_from_left(V.y)};
+        const f32x2 yv =
+            f32x2{lane_from_left(D.x) + lane_from_right(D.x), lane_from_left(D.y) + lane_from_right(D.y)} + 2.0f * D;
+        const f32x2 n2 = x * x + yv * yv + 1e-8f;
+        const f32x2 inv = f32x2{__builtin_amdgcn_rsqf(n2.x), __builtin_amdgcn_rsqf(n2.y)};
+        const f32x2 gx = x * inv, gy = yv * inv;
+        const f32x2 res =
+            (half(t[qq][0]) * pw.w0 + half(t[qq][1]) * pw.w1 + half(t[qq][2]) * pw.w2 + half(t[qq][3]) * pw.w3) - c;
+        Q[0] += gx * gx;
+        Q[1] += gx * gy;
+        Q[2] += gy * gy;
+        Q[3] += gx * res;
+        Q[4] += gy * res;
+        Q[5] += res * res;
+        Q[6] += gx;
+        Q[7] += gy;
+        Q[8] += res;
       }
     }
+#pragma unroll
+    for (int i = 0; i < 9; ++i) qs[par][wave][i][lane] = Q[i].x + Q[i].y;
+    // occlusion / masks / sigma terms (every wave, same values)
+    const float d1w = bilp(gd1, pw);
+    const bool ok = (fw.iz > d1w - 0.1f) && (fw.u > 0.0f) && (fw.u < (float)W) && (fw.v > 0.0f) && (fw.v < (float)H);
+    bool invalid = !ok || !out_lane || !fm0 || !(fm1 > 0.0f);
+    float A = 1.0f, bx = 0.0f, by = 0.0f, sr0 = 0.0f;
+    if (!NOSIG) {
+      float hx, hy;
+      sobel_cols(s0t, s0m, s0b, hx, hy);
+      sr0 = bilp(gs1, pw);
+      const float sg = sqrtf(sr0 * sr0 + s0m * s0m);
+      A = __builtin_amdgcn_rcpf(sg);
+      const float kk = s0m * (A * A * A);
+      bx = kk * hx;
+      by = kk * hy;
+      if (TRU) invalid = invalid || (s0m == g0min) || (s0m == g0max);
+    }
+    __syncthreads();  // qs[par] complete; the other buffer is free for the next unit
+    if (out_lane) {
+      float q[9];
+#pragma unroll
+      for (int i = 0; i < 9; ++i)
+        q[i] = ((qs[par][0][i][lane] + qs[par][1][i][lane]) + qs[par][2][i][lane]) + qs[par][3][i][lane];
+      const float A2 = A * A;
+      const float Saa = A2 * q[0] + 2.0f * A * bx * q[3] + bx * bx * q[5];
+      const float Sab = A2 * q[1] + A * by * q[3] + A * bx * q[4] + bx * by * q[5];
+      const float Sbb = A2 * q[2] + 2.0f * A * by * q[4] + by * by * q[5];
+      const float Sa = -(A * q[6] + bx * q[8]), Sb = -(A * q[7] + by * q[8]);
+      const float Sar = -(A2 * q[3] + A * bx * q[5]), Sbr = -(A2 * q[4] + A * by * q[5]);
+      float Jx[6], Jy[6];
+      warp_jac(fw.xr, fw.yr, d, fx, fy, Jx, Jy);
+      acc.add(wave, lane, Saa, Sab, Sbb, Sa, Sb, Sar, Sbr, Jx, Jy, invalid, sr0, lds_ext);
+    }
   }
-  __syncthreads();
-  float* out = p.rec + (size_t)kb * kRec;
-  const int tid = threadIdx.x;
-  if (tid < (TRU ? R_NMX + 1 : R_NINV + 1)) st_ag(out + tid, red[tid]);
+  acc.write_record(wave, lane, lds_ext, red, p.rec + (size_t)kb * kRec);
   if (p.fin_on && block_is_last(p.fin.pair_cnt + b, 1u, (uint32_t)p.nbpp)) {
     pair_reduce(p.fin, b);
     if (block_is_last(p.fin.done_cnt, 1u, (uint32_t)p.B)) finalize_batch(p.fin);
@@ -2557,7 +2590,7 @@ int launch_minmax(const DpftLevelDesc& d, const DpftLevelTensors& tt, void* ws, 
 }
 
 // Workgroups of `kernel` the current device holds at once (cached per kernel and device).
-int resident_blocks(const void* kernel) {
+int resident_blocks(const void* kernel, int threads = kThreads) {
   struct Entry {
     const void* k;
     int dev, n;
@@ -2570,7 +2603,7 @@ int resident_blocks(const void* kernel) {
   for (const Entry& e : cache)
     if (e.k == kernel && e.dev == dev) return e.n;
   int per_cu = 0, cus = 0;
-  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kernel, kThreads, 0) != hipSuccess ||
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kernel, threads, 0) != hipSuccess ||
       hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
     return 0;
   const int n = std::max(1, std::min(per_cu * cus, kMaxGrid));
@@ -2583,14 +2616,13 @@ int launch_reduce_k(IterParams p, hipStream_t st) {
   const void* k = reinterpret_cast<const void*>(&ic_reduce_kernel<CT, CS1, TRU, MODE, C4>);
   const int cap = resident_blocks(k);
   if (cap <= 0) return fail(DPFT_E_HIP, "occupancy query failed");
-#ifdef DPFT_GRID_DIV
-  const int capd = cap / DPFT_GRID_DIV;
-#else
-  const int capd = cap;
-#endif
-  p.nbpp = std::max(1, std::min(capd / p.B, p.per_pair));
+  p.nbpp = std::max(1, std::min(cap / p.B, p.per_pair));
   p.fin.nbpp = p.nbpp;
+  // finalize in-kernel (last-workgroup handshake) or as its own one-workgroup launch
+  const bool sep = p.fin_on && (long)p.H * p.W <= kSepFinMaxPixels;
+  if (sep) p.fin_on = 0;
   hipLaunchKernelGGL((ic_reduce_kernel<CT, CS1, TRU, MODE, C4>), dim3(p.B * p.nbpp), dim3(kThreads), 0, st, p);
+  if (sep) hipLaunchKernelGGL(finalize_kernel, dim3(p.B), dim3(kThreads), 0, st, p.fin);
   return DPFT_OK;
 }
 
@@ -2611,30 +2643,36 @@ int launch_reduce_t(const IterParams& p, hipStream_t st) {
 }
 
 template <int CT, bool TRU, int MODE>
-int launch_wgmarch(IterParams p, hipStream_t st) {
-  const void* k = reinterpret_cast<const void*>(&ic_wgmarch_kernel<CT, TRU, MODE>);
+int launch_split(IterParams p, hipStream_t st) {
+  const void* k = reinterpret_cast<const void*>(&ic_split_kernel<CT, TRU, MODE>);
   const int cap = resident_blocks(k);
   if (cap <= 0) return fail(DPFT_E_HIP, "occupancy query failed");
-#ifdef DPFT_GRID_DEN
-  const int capd = cap * DPFT_GRID_NUM / DPFT_GRID_DEN;
-#else
-  const int capd = cap;
-#endif
-  // at least ~4 rows per workgroup (the row pipeline is two rows deep)
   const int units = p.tiles_x * p.H;
-  p.nbpp = std::max(1, std::min(capd / p.B, units / 4));
+  p.nbpp = std::max(1, std::min(cap / p.B, units));
   p.fin.nbpp = p.nbpp;
-  hipLaunchKernelGGL((ic_wgmarch_kernel<CT, TRU, MODE>), dim3(p.B * p.nbpp), dim3(kThreads), 0, st, p);
+  // Many small workgroups finish together here: the last-block handshake would
+  // serialise B * nbpp atomics on B counters, so the finalize is its own launch
+  // (B workgroups, the kernel boundary orders the records).
+  const bool sep = kSplitSepFin && p.fin_on;
+  if (sep) p.fin_on = 0;
+  hipLaunchKernelGGL((ic_split_kernel<CT, TRU, MODE>), dim3(p.B * p.nbpp), dim3(kThreads), 0, st, p);
+  if (sep) hipLaunchKernelGGL(finalize_kernel, dim3(p.B), dim3(kThreads), 0, st, p.fin);
   return DPFT_OK;
 }
 
 template <int CT>
 int launch_reduce_c4(const IterParams& p, hipStream_t st) {
   const bool tru = (p.flags & DPFT_REMOVE_TRU_SIGMA) != 0;
-  if constexpr (kWgMarch && CT > 0 && CT % 16 == 0) {
-    if (p.flags & DPFT_NO_UNCERTAINTY) return launch_wgmarch<CT, false, 2>(p, st);
-    if (!(p.flags & DPFT_COMBINE_ICP))
-      return tru ? launch_wgmarch<CT, true, 0>(p, st) : launch_wgmarch<CT, false, 0>(p, st);
+  if constexpr (CT > 0 && CT % 16 == 0) {
+    uint32_t sched = p.flags & DPFT_SCHED_MASK;
+    if (sched == DPFT_SCHED_AUTO)  // coarse levels (few pixels per pair): the channel-split kernel
+      sched = ((long)p.H * p.W <= kSplitMaxPixels) ? DPFT_SCHED_SPLIT : DPFT_SCHED_MARCH;
+    if (!(p.flags & DPFT_COMBINE_ICP)) {  // combine_ICP: ic_reduce_kernel (marching path)
+      if (sched == DPFT_SCHED_SPLIT) {
+        if (p.flags & DPFT_NO_UNCERTAINTY) return launch_split<CT, false, 2>(p, st);
+        return tru ? launch_split<CT, true, 0>(p, st) : launch_split<CT, false, 0>(p, st);
+      }
+    }
   }
   if (p.flags & DPFT_NO_UNCERTAINTY) return launch_reduce_k<CT, true, false, 2, true>(p, st);
   if (p.flags & DPFT_COMBINE_ICP)

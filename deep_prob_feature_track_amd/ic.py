@@ -100,11 +100,14 @@ class LevelCall:
     """Validated, pointer-ready arguments of one pyramid level.
 
     x0 / x1 are [B,C,H,W] (NCHW) or channel-quad packed [B,C/4,H,W,4]; with
-    pack=True eligible NCHW inputs are packed here (once for all iterations)."""
+    pack=True eligible NCHW inputs are packed here (once for all iterations).
+    schedule (None = "auto", "march", "split") forces the channel-quad
+    reduce kernel (include/dpft_ic.h, DPFT_SCHED_*); it changes only the order in
+    which the per-pixel sums are added."""
 
     def __init__(self, x0, x1, invD0, invD1, K, sigma0, sigma1, iters=3, remove_tru_sigma=False,
                  obj_mask0=None, obj_mask1=None, depth0=None, depth1=None, combine_icp=False,
-                 icp_weight=0.01, status=None, no_uncertainty=False, pack=False):
+                 icp_weight=0.01, status=None, no_uncertainty=False, pack=False, schedule=None):
         if not x0.is_cuda:
             raise RuntimeError("the HIP solver needs device tensors (got CPU); there is no CPU fallback")
         for name, t in (("x0", x0), ("x1", x1), ("invD0", invD0), ("invD1", invD1), ("K", K)):
@@ -143,6 +146,10 @@ class LevelCall:
             flags |= N.FEATURES_C4
         if no_uncertainty:
             flags |= N.NO_UNCERTAINTY
+        if schedule is not None:  # channel-quad reduce kernel override (tests / tuning)
+            if schedule not in N.SCHEDULES:
+                raise ValueError(f"schedule must be one of {sorted(N.SCHEDULES)} (got {schedule!r})")
+            flags |= N.SCHEDULES[schedule]
         if combine_icp:
             if depth0 is None or depth1 is None:
                 raise ValueError("combine_icp needs depth0 and depth1")
@@ -281,7 +288,8 @@ class PyramidSolver:
     obj_mask1, depth0, depth1]); K is the level-0 intrinsics [B,4].
     """
 
-    def __init__(self, levels, K, iters=3, remove_tru_sigma=False, combine_icp=False, icp_weight=0.01):
+    def __init__(self, levels, K, iters=3, remove_tru_sigma=False, combine_icp=False, icp_weight=0.01,
+                 schedule=None):
         dev = levels[0]["x0"].device
         self.status = torch.zeros(1, dtype=torch.int32, device=dev)
         self.calls = []
@@ -290,7 +298,7 @@ class PyramidSolver:
                                         d["sigma0"], d["sigma1"], iters=iters, remove_tru_sigma=remove_tru_sigma,
                                         obj_mask0=d.get("obj_mask0"), obj_mask1=d.get("obj_mask1"),
                                         depth0=d.get("depth0"), depth1=d.get("depth1"), combine_icp=combine_icp,
-                                        icp_weight=icp_weight, status=self.status))
+                                        icp_weight=icp_weight, status=self.status, schedule=schedule))
         nbytes = max(c.ws_bytes for c in self.calls)
         self.ws = torch.zeros(nbytes, dtype=torch.uint8, device=dev)  # private: safe to capture; zeroed (counters)
         self.ws_bytes = nbytes

@@ -62,6 +62,17 @@ extern "C" {
                                       (or NO_UNCERTAINTY).  Same values, coalesced
                                       16-byte loads of 4 channels per pixel / tap.    */
 
+/* Channel-quad reduce schedule (bits 4-5; FEATURES_C4 with C = 16 or 32 only, else
+   ignored).  AUTO picks per level; the others force one kernel -- same arithmetic,
+   a different summation grouping -- for tests and tuning:
+     MARCH   a wave walks a band of rows of one 62-column strip with a window of f0 rows
+     SPLIT   a workgroup per (strip, row), the 4 waves split the channel quads
+             (AUTO: levels of at most 40000 pixels per pair) */
+#define DPFT_SCHED_MASK    0x30u
+#define DPFT_SCHED_AUTO    0x00u
+#define DPFT_SCHED_MARCH   0x10u
+#define DPFT_SCHED_SPLIT   0x20u
+
 /* device status word bits */
 #define DPFT_STATUS_NONFINITE 0x1u /* a JtJ / JtR reduction was not finite         */
 

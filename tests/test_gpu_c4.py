@@ -150,3 +150,76 @@ def test_c4_rejects_per_channel_sigma():
     pose = (torch.eye(3, device=dev)[None], torch.zeros(1, 3, 1, device=dev))
     with pytest.raises(ValueError, match="single sigma plane"):
         ic.solve_level(pose, x, x, d, d, K, s, s)
+
+
+SCHEDULES = ["march", "split"]
+
+
+@pytest.mark.parametrize("schedule", SCHEDULES)
+def test_c4_schedules_from_reference_pose(schedule):
+    """cfg2 (C = 32, 4 levels): every reduce schedule, re-started from the reference's
+    pose of the previous iteration, gives the reference's invalid count exactly and the
+    NCHW kernel's normal equations (summation-order noise only)."""
+    from deep_prob_feature_track_amd import ic
+    dev = _dev()
+    case, z = golden_io.load("cfg2_640x480_c32")
+    lv = golden_io.levels_torch(case, torch.float32, dev)
+    R0, t0 = golden_io.init_pose(case, torch.float32, dev)
+    K = torch.from_numpy(case["K"]).to(dev)
+    i = 0
+    for l in reversed(range(case["levels"])):
+        d = lv[l]
+        packed = (ic.pack_features(d["f0"]), ic.pack_features(d["f1"]))
+        for it in range(3):
+            R = torch.from_numpy(z["f32_R"][i - 1]).to(dev) if i else R0
+            t = (torch.from_numpy(z["f32_t"][i - 1]).to(dev) if i else t0).reshape(-1, 3, 1)
+            out = []
+            for (f0, f1), kw in (((d["f0"], d["f1"]), {}), (packed, dict(schedule=schedule))):
+                o = ic.iterate((R, t), f0, f1, d["invD0"], d["invD1"], K / 2 ** l, d["s0"], d["s1"], first=True,
+                               remove_tru_sigma=bool(z["opt_remove_tru_sigma"]), **kw)
+                out.append([x.cpu().numpy() for x in o])
+            (Ra, ta, ja, ra, na), (Rb, tb, jb, rb, nb) = out
+            assert (na == nb).all() and (nb == z["f32_invalid"][i]).all(), f"iter {i}: {na} {nb}"
+            assert np.abs(ja - jb).max() / np.abs(ja).max() < 1e-6, f"iter {i}"
+            assert np.abs(ra - rb).max() / np.abs(ra).max() < 1e-4, f"iter {i}"
+            for prec in ("f32", "f64"):
+                assert np.abs(Rb - z[f"{prec}_R"][i]).max() <= SE3_TOL, f"iter {i} vs {prec}"
+                assert np.abs(tb.reshape(-1, 3) - z[f"{prec}_t"][i]).max() <= SE3_TOL, f"iter {i} vs {prec}"
+            i += 1
+
+
+@pytest.mark.parametrize("schedule", SCHEDULES)
+@pytest.mark.parametrize("C,H,W,no_unc,masks", [(32, 37, 70, False, True), (16, 61, 129, True, False),
+                                                 (32, 3, 2, False, False), (16, 130, 63, False, True)])
+def test_c4_schedules_random(schedule, C, H, W, no_unc, masks):
+    """Ragged strips (W not a multiple of 62), tiny levels (H = 3, W = 2), masks, IC and
+    U_IC with truncated sigma: each schedule against the NCHW kernel."""
+    from deep_prob_feature_track_amd import ic
+    dev = _dev()
+    g = torch.Generator().manual_seed(C * 1000 + H)
+    B = 3
+    f0 = torch.rand(B, C, H, W, generator=g)
+    f1 = torch.roll(f0, shifts=(1, 2), dims=(2, 3)) + 0.01 * torch.rand(B, C, H, W, generator=g)
+    s0 = 0.5 + torch.rand(B, 1, H, W, generator=g)
+    s1 = 0.5 + torch.rand(B, 1, H, W, generator=g)
+    d0 = 0.2 + torch.rand(B, 1, H, W, generator=g)
+    d1 = 0.2 + torch.rand(B, 1, H, W, generator=g)
+    m0 = torch.rand(B, 1, H, W, generator=g) > 0.1
+    m1 = torch.rand(B, 1, H, W, generator=g) > 0.2
+    K = torch.tensor([[W * 0.8, W * 0.8, (W - 1) / 2, (H - 1) / 2]]).repeat(B, 1)
+    f0, f1, s0, s1, d0, d1, m0, m1, K = [v.to(dev) for v in (f0, f1, s0, s1, d0, d1, m0, m1, K)]
+    R = torch.eye(3, device=dev).repeat(B, 1, 1)
+    R[:, 0, 1], R[:, 1, 0] = 0.01, -0.01
+    t = torch.full((B, 3, 1), 0.003, device=dev)
+    kw = dict(no_uncertainty=True) if no_unc else dict(remove_tru_sigma=True)
+    if masks:
+        kw.update(obj_mask0=m0, obj_mask1=m1)
+    sa, sb = (None, None) if no_unc else (s0, s1)
+    a = ic.iterate((R, t), f0, f1, d0, d1, K, sa, sb, first=True, **kw)
+    b = ic.iterate((R, t), ic.pack_features(f0), ic.pack_features(f1), d0, d1, K, sa, sb, first=True,
+                   schedule=schedule, **kw)
+    assert torch.equal(a[4], b[4])  # invalid counts
+    torch.testing.assert_close(b[2], a[2], rtol=2e-6, atol=1e-6 * a[2].abs().max().item())
+    torch.testing.assert_close(b[3], a[3], rtol=1e-4, atol=1e-5 * a[3].abs().max().item())
+    torch.testing.assert_close(b[0], a[0], rtol=0, atol=2e-5)
+    torch.testing.assert_close(b[1], a[1], rtol=0, atol=2e-5)

@@ -18,13 +18,14 @@ p.add_argument("--batch", type=int, default=8)
 p.add_argument("--reps", type=int, default=20)
 p.add_argument("--mode", choices=["reduce", "iterate"], default="reduce")
 p.add_argument("--c4", action="store_true", help="channel-quad packed features")
+p.add_argument("--schedule", default=None, help="auto | march | split (channel-quad reduce kernel)")
 a = p.parse_args()
 dev = torch.device("cuda:0")
 sel, levels, K = bench.make_inputs(a.batch, 0, dev)
 if a.c4:
     for d in levels:
         d["x0"], d["x1"] = ic.pack_features(d["x0"]), ic.pack_features(d["x1"])
-solver = ic.PyramidSolver(levels, K, iters=3, remove_tru_sigma=True)
+solver = ic.PyramidSolver(levels, K, iters=3, remove_tru_sigma=True, schedule=a.schedule)
 R = torch.eye(3, device=dev).repeat(a.batch, 1, 1).contiguous()
 t = torch.zeros(a.batch, 3, device=dev)
 import ctypes
@@ -46,5 +47,5 @@ for level in ([a.level] if a.level >= 0 else range(len(solver.calls))):
     torch.cuda.synchronize()
     us = e0.elapsed_time(e1) / a.reps * 1e3
     gbs = solver.algorithmic_bytes(level) / (us * 1e-6) / 1e9
-    print(f"{os.path.basename(os.environ.get('DPFT_LIB', 'libdpft_ic.so'))}{' c4' if a.c4 else ''} {a.mode} level {level} B={a.batch}: "
+    print(f"{os.path.basename(os.environ.get('DPFT_LIB', 'libdpft_ic.so'))}{' c4' if a.c4 else ''}{' ' + a.schedule if a.schedule else ''} {a.mode} level {level} B={a.batch}: "
           f"{us:.1f} us/launch, {gbs:.0f} GB/s algorithmic ({gbs / 80:.1f}% of 8 TB/s)", flush=True)
