@@ -69,6 +69,21 @@ def make_inputs(B, rank, device):
     return sel, levels, K
 
 
+def l0_traffic():
+    """Per-launch HBM bytes of the level-0 reduce launch from the committed PMC
+    measurement (tools/pmc_l0.py: separate FETCH_SIZE / WRITE_SIZE rocprofv3 passes,
+    gfx950-corrected), used only if it was measured on the kernel source built here."""
+    import glob
+    import hashlib
+    src = os.path.join(ROOT, "deep_prob_feature_track_amd", "csrc", "dpft_ic.hip")
+    sha = hashlib.sha256(open(src, "rb").read()).hexdigest()
+    for f in sorted(glob.glob(os.path.join(ROOT, "profiles", "*_l0_traffic.json")), reverse=True):
+        d = json.load(open(f))
+        if d.get("src_sha256") == sha:
+            return {"hbm_bytes": d["hbm_bytes"], "source": os.path.relpath(f, ROOT)}
+    return None
+
+
 def cpu_baseline(levels_gpu, K, R_gpu, t_gpu):
     """Oracle (PyTorch-CPU restatement of the reference solver) on pair 0: 1 warm-up, best of 2."""
     from oracle import ic_oracle as O
@@ -128,17 +143,16 @@ def main():
         return e0.elapsed_time(e1) / reps * 1e3
 
     levels = packed(levels_nchw) if a.layout == "c4" else levels_nchw
-    R_init = torch.eye(3, device=device).repeat(B, 1, 1).contiguous()
-    t_init = torch.zeros(B, 3, device=device)
+    # R [B,3,3] and t [B,3] as two contiguous views of one buffer: one reset copy per step
+    pose_init = torch.cat((torch.eye(3, device=device).repeat(B, 1, 1).reshape(-1), torch.zeros(B * 3, device=device)))
 
     def make_step(levels):
         solver = ic.PyramidSolver(levels, K, iters=ITERS, remove_tru_sigma=True)
-        R = R_init.clone()
-        t = t_init.clone()
+        pose = pose_init.clone()
+        R, t = pose[:9 * B].view(B, 3, 3), pose[9 * B:].view(B, 3)
 
         def solve():
-            R.copy_(R_init)
-            t.copy_(t_init)
+            pose.copy_(pose_init)
             solver.run(R, t)
 
         # eager warm-up (also validates), then capture the whole 4-level solve into one graph
@@ -215,6 +229,7 @@ def main():
     kern_us = ev0.elapsed_time(ev1) / a.kernel_reps * 1e3
     alg_bytes = solver.algorithmic_bytes(0)
     achieved = alg_bytes / (kern_us * 1e-6) / 1e9
+    traffic = l0_traffic() if a.layout == "c4" and B == 8 else None
 
     # secondary (rank 0 only, not the headline): the same solve from the other resident
     # layout, and the one-time cost of packing NCHW pyramids into the channel-quad layout
@@ -260,7 +275,9 @@ def main():
             "pairs_per_s": world * B * a.steps / elapsed,
             "l0_iters_per_s": world * B * ITERS * a.steps / elapsed,
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                         "frac": achieved / HBM_PEAK_GBS, "traffic": None,
+                         "frac": achieved / HBM_PEAK_GBS,
+                         "traffic": traffic["hbm_bytes"] if traffic else None,
+                         "traffic_source": traffic["source"] if traffic else None,
                          "kernel": f"ic_reduce_kernel<32,Cs=1,tru,U_IC,{a.layout}> (level 0, + in-kernel finalize)",
                          "kernel_us": kern_us, "algorithmic_bytes_per_launch": alg_bytes},
             "cpu_baseline": cpu,

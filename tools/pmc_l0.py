@@ -1,0 +1,65 @@
+#!/usr/bin/env python
+"""HBM traffic of the level-0 reduce launch from rocprofv3 PMC passes (run on the GPU box).
+
+    python tools/pmc_l0.py --out profiles/r1_l0_traffic.json
+
+Runs tools/kbench.py (level 0, channel-quad, `iterate` = the launch bench.py times)
+under two separate `rocprofv3 --pmc` passes (FETCH_SIZE; WRITE_SIZE) and writes the
+per-launch bytes, corrected as MI355X_MICROARCH.md's HBM section prescribes:
+FETCH_SIZE counts half the bytes of a 128-B-request stream on gfx950 (TCC_EA0_RDREQ
+x 64 B) -> read bytes = 2 x 1024 x FETCH_SIZE; WRITE_SIZE (KiB) is exact.  The
+JSON carries the SHA-256 of the kernel source, so bench.py uses it only while the
+source it was measured on is unchanged.
+"""
+import argparse
+import csv
+import glob
+import hashlib
+import json
+import os
+import subprocess
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+SRC = os.path.join(ROOT, "deep_prob_feature_track_amd", "csrc", "dpft_ic.hip")
+
+
+def src_sha():
+    return hashlib.sha256(open(SRC, "rb").read()).hexdigest()
+
+
+def run_pass(counter, outdir):
+    cmd = ["timeout", "-s", "KILL", "90", "rocprofv3", "--pmc", counter, "--output-format", "csv", "-d", outdir,
+           "-o", "c", "--", sys.executable, os.path.join(ROOT, "tools", "kbench.py"), "--c4", "--level", "0",
+           "--mode", "iterate", "--reps", "10"]
+    subprocess.run(cmd, check=True, cwd="/tmp", env=dict(os.environ, TMPDIR="/tmp"))
+    vals = []
+    for f in glob.glob(os.path.join(outdir, "**", "*counter_collection.csv"), recursive=True):
+        for r in csv.DictReader(open(f)):
+            if "ic_reduce_kernel" in r["Kernel_Name"] and r["Counter_Name"] == counter:
+                vals.append(float(r["Counter_Value"]))
+    if not vals:
+        raise SystemExit(f"no ic_reduce_kernel rows for {counter}")
+    return sum(vals) / len(vals), len(vals)
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--out", required=True)
+    a = ap.parse_args()
+    tmp = os.path.join(ROOT, "gpurun_out", "pmc_l0")
+    fetch, nf = run_pass("FETCH_SIZE", os.path.join(tmp, "fetch"))
+    write, nw = run_pass("WRITE_SIZE", os.path.join(tmp, "write"))
+    out = {"kernel": "ic_reduce_kernel<32,Cs=1,tru,U_IC,c4> level 0, B=8, 640x480 (tools/kbench.py --mode iterate)",
+           "src_sha256": src_sha(), "launches": {"fetch": nf, "write": nw},
+           "FETCH_SIZE_KiB": fetch, "WRITE_SIZE_KiB": write,
+           "read_bytes": 2 * 1024 * fetch, "write_bytes": 1024 * write,
+           "hbm_bytes": 2 * 1024 * fetch + 1024 * write,
+           "correction": "read = 2 x 1024 x FETCH_SIZE (gfx950 tallies 128-B read requests at 64 B), "
+                         "write = 1024 x WRITE_SIZE"}
+    json.dump(out, open(a.out, "w"), indent=1)
+    print(json.dumps(out))
+
+
+if __name__ == "__main__":
+    main()

@@ -1,90 +1,93 @@
 #!/usr/bin/env python
-"""Summarise rocprofv3 CSV output per (kernel, grid) and derive per-launch HBM traffic.
+"""Per-level summary of a bench.py rocprofv3 kernel trace (+ optional PMC passes).
 
-usage: python tools/prof_summary.py --trace DIR/x_kernel_trace.csv \
-           [--fetch DIR/fetch_counter_collection.csv] [--write ...] [--hit ...] \
-           --out profiles/r1_summary  (writes .md and .json)
+usage: python tools/prof_summary.py --trace DIR/bench_kernel_trace.csv \
+           [--traffic profiles/r1_l0_traffic.json] --out profiles/r1_summary [--title T]
 
-rocprofv3 --stats averages a kernel over every launch of that symbol, and the solver
-launches the same `ic_reduce_kernel<32,true,true>` instantiation at all four pyramid
-levels; the per-grid split below separates level 0 (the roofline kernel) from the rest.
-FETCH_SIZE / WRITE_SIZE are in KiB; on gfx950 FETCH_SIZE counts half the bytes of a
-coalesced read (MI355X_MICROARCH.md, HBM section) -- we calibrated the same factor on
-minmax_kernel, a plain 4 B/lane streaming read of a known byte count -- so HBM read
-bytes = 2 * 1024 * FETCH_SIZE.
+Every launch is assigned to a pyramid level by the sigma0 min/max pass that opens the
+level (its grid is the level's size: smallest = level 3), and to the feature layout
+(channel-quad kernels carry `true>` / are the split kernel; the NCHW comparison solve
+`false>`).  Writes <out>.md and <out>.json: per (layout, level, kernel) the number of
+launches and their average / min / max duration, and one solve's timeline.
 """
 import argparse
 import collections
 import csv
 import json
+import re
 
 
 def short(name):
-    n = name.replace("(anonymous namespace)::", "")
-    return n.split("(")[0] if not n.startswith("void ") else n[5:].split("(")[0]
-
-
-def trace_groups(path):
-    g = collections.defaultdict(list)
-    for r in csv.DictReader(open(path)):
-        grid = int(r.get("Grid_Size_X") or r.get("Grid_Size"))
-        wg = int(r.get("Workgroup_Size_X") or r.get("Workgroup_Size"))
-        g[(short(r["Kernel_Name"]), grid // max(wg, 1))].append(
-            (int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e3)
-    return g
-
-
-def counter_groups(path):
-    g = collections.defaultdict(list)
-    for r in csv.DictReader(open(path)):
-        grid = int(r["Grid_Size"]) // max(int(r["Workgroup_Size"]), 1)
-        g[(short(r["Kernel_Name"]), grid, r["Counter_Name"])].append(float(r["Counter_Value"]))
-    return g
+    n = name.replace("(anonymous namespace)::", "").replace("void ", "")
+    m = re.match(r"([A-Za-z_0-9]+(<[^>]*>)?)", n)
+    return m.group(1) if m else n[:60]
 
 
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--trace", required=True)
-    ap.add_argument("--fetch")
-    ap.add_argument("--write")
-    ap.add_argument("--hit")
+    ap.add_argument("--traffic")
     ap.add_argument("--out", required=True)
     ap.add_argument("--title", default="")
     a = ap.parse_args()
-    tg = trace_groups(a.trace)
-    cg = collections.defaultdict(list)
-    for p in (a.fetch, a.write, a.hit):
-        if p:
-            for k, v in counter_groups(p).items():
-                cg[k] += v
-    rows = []
-    for (k, blocks), d in sorted(tg.items(), key=lambda kv: -sum(kv[1])):
-        row = {"kernel": k, "workgroups": blocks, "calls": len(d), "avg_us": sum(d) / len(d),
-               "min_us": min(d), "max_us": max(d), "total_us": sum(d)}
-        def mean(c):
-            v = cg.get((k, blocks, c))
-            return sum(v) / len(v) if v else None
-        f, w = mean("FETCH_SIZE"), mean("WRITE_SIZE")
-        h, m = mean("TCC_HIT_sum"), mean("TCC_MISS_sum")
-        if f is not None:
-            row["hbm_read_bytes"] = 2 * 1024 * f
-        if w is not None:
-            row["hbm_write_bytes"] = 1024 * w
-        if h is not None and m is not None and h + m > 0:
-            row["l2_hit_rate"] = h / (h + m)
-        rows.append(row)
-    json.dump(rows, open(a.out + ".json", "w"), indent=1)
-    with open(a.out + ".md", "w") as fo:
-        fo.write(f"# {a.title}\n\n" if a.title else "")
-        fo.write("| kernel | workgroups | calls | avg us | min us | max us | HBM read MB/launch | HBM write MB/launch | L2 hit |\n")
-        fo.write("|---|---|---|---|---|---|---|---|---|\n")
-        for r in rows:
-            rd = f"{r['hbm_read_bytes'] / 1e6:.1f}" if "hbm_read_bytes" in r else ""
-            wr = f"{r['hbm_write_bytes'] / 1e6:.3f}" if "hbm_write_bytes" in r else ""
-            hr = f"{r['l2_hit_rate']:.3f}" if "l2_hit_rate" in r else ""
-            fo.write(f"| {r['kernel']} | {r['workgroups']} | {r['calls']} | {r['avg_us']:.1f} | {r['min_us']:.1f} | "
-                     f"{r['max_us']:.1f} | {rd} | {wr} | {hr} |\n")
-    print(open(a.out + ".md").read())
+    rows = sorted(csv.DictReader(open(a.trace)), key=lambda r: int(r["Start_Timestamp"]))
+    mm_grids = sorted({int(r["Grid_Size_X"]) for r in rows if "minmax" in r["Kernel_Name"]})
+    level_of_grid = {g: len(mm_grids) - 1 - i for i, g in enumerate(mm_grids)}
+    groups = collections.defaultdict(list)
+    level = None
+    timeline, cur, solves = [], [], []
+    for r in rows:
+        name = short(r["Kernel_Name"])
+        dur = (int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e3
+        if "minmax" in name:
+            level = level_of_grid[int(r["Grid_Size_X"])]
+            if level == len(mm_grids) - 1 and cur:
+                solves.append(cur)
+                cur = []
+        if level is None:
+            continue
+        layout = "nchw" if name.endswith("false>") else "c4"
+        if name.startswith(("ic_reduce", "ic_split", "finalize", "minmax")):
+            groups[(layout if not name.startswith(("finalize", "minmax")) else "-", level, name)].append(dur)
+        cur.append((int(r["Start_Timestamp"]), dur, level, name, int(r["Grid_Size_X"]) // max(int(r["Workgroup_Size_X"]), 1)))
+    # one channel-quad solve: the last complete one whose reduce launches are channel-quad
+    c4 = [s for s in solves if any(n.endswith("true>") or n.startswith("ic_split") for _, _, _, n, _ in s)]
+    one = c4[-1] if c4 else []
+    # cut after the level-0 iterations of the solve (bench.py times extra level-0 launches after it)
+    n0, cut = 0, len(one)
+    for i, (_, _, lv, name, _) in enumerate(one):
+        if lv == 0 and name.startswith(("ic_reduce", "ic_split")):
+            n0 += 1
+            if n0 == 3:
+                cut = i + 1
+                break
+    one = one[:cut]
+    out = {"levels": {}, "timeline": []}
+    lines = [f"# {a.title}\n" if a.title else "", "## Launches per level (all solves in the trace)\n",
+             "| layout | level | kernel | launches | avg us | min us | max us |", "|---|---|---|---|---|---|---|"]
+    for (layout, lv, name), d in sorted(groups.items(), key=lambda kv: (kv[0][0], -kv[0][1], kv[0][2])):
+        lines.append(f"| {layout} | {lv} | {name} | {len(d)} | {sum(d) / len(d):.1f} | {min(d):.1f} | {max(d):.1f} |")
+        out["levels"][f"{layout}/L{lv}/{name}"] = {"launches": len(d), "avg_us": sum(d) / len(d),
+                                                   "min_us": min(d), "max_us": max(d)}
+    if one:
+        t0 = one[0][0]
+        lines += ["", "## One channel-quad solve (B = 8 pairs, graph replay)\n",
+                  "| start us | duration us | level | kernel | workgroups |", "|---|---|---|---|---|"]
+        for st, d, lv, name, wg in one:
+            lines.append(f"| {(st - t0) / 1e3:.1f} | {d:.1f} | {lv} | {name} | {wg} |")
+            out["timeline"].append({"start_us": (st - t0) / 1e3, "us": d, "level": lv, "kernel": name, "wg": wg})
+        wall = (one[-1][0] - t0) / 1e3 + one[-1][1]
+        lines.append(f"\nsolve wall {wall:.1f} us, kernel sum {sum(x[1] for x in one):.1f} us")
+        out["solve_wall_us"] = wall
+    if a.traffic:
+        t = json.load(open(a.traffic))
+        out["l0_traffic"] = t
+        lines += ["", "## Level-0 reduce launch: HBM traffic (separate FETCH_SIZE / WRITE_SIZE passes)\n",
+                  f"read {t['read_bytes'] / 1e6:.1f} MB + write {t['write_bytes'] / 1e6:.2f} MB per launch "
+                  f"({t['correction']}); algorithmic 668.5 MB -> {t['hbm_bytes'] / 668467200:.2f}x"]
+    open(a.out + ".md", "w").write("\n".join(lines) + "\n")
+    json.dump(out, open(a.out + ".json", "w"), indent=1)
+    print("\n".join(lines))
 
 
 if __name__ == "__main__":
