@@ -113,6 +113,10 @@ constexpr long kSepFinMaxPixels = DPFT_SEPFIN_MAX_PIXELS;  // ic_reduce_kernel l
 #ifndef DPFT_MARCH_ROWS
 #define DPFT_MARCH_ROWS 1
 #endif
+#ifndef DPFT_MARCH_CSPLIT
+#define DPFT_MARCH_CSPLIT 1
+#endif
+constexpr int kMarchCSplit = DPFT_MARCH_CSPLIT;  // waves sharing a marching band (channel quads split)
 constexpr int kMarchRows = DPFT_MARCH_ROWS;  // rows per marching step (1, or 2: -10 % f1 traffic, +11 % VALU, 4 % slower)
 constexpr int kRingM = DPFT_RING_M;       // quads in flight on the marching path (kRingM - 1 ahead)
 #ifndef DPFT_F0_AUX
@@ -1063,7 +1067,7 @@ __global__ __launch_bounds__(kThreads, DPFT_MIN_WAVES) void ic_reduce_kernel(Ite
   __shared__ float lds_ext[TRU ? 2 * 7 : 1][kThreads];  // extremum corrections (6 + count), min then max
   __shared__ float red[4][kRec];
   constexpr bool kWin = C4 && kMarch && CT > 0;
-  __shared__ f32x4 lds_win[kWin ? 4 : 1][kWin ? 2 * (CT / 4) * 64 : 1];
+  __shared__ f32x4 lds_win[kWin ? 4 : 1][kWin ? 2 * (CT / 4) * 64 : 1];  // used: 2 x NQW quads per wave
 
   const int tid = threadIdx.x, lane = tid & 63, wave = wave_id();
   const int W = p.W, H = p.H, HW = H * W;
@@ -1203,6 +1207,9 @@ __global__ __launch_bounds__(kThreads, DPFT_MIN_WAVES) void ic_reduce_kernel(Ite
     }
   };
 
+  // Per-pixel counts (invalid pixels, truncated-sigma extremum pixels) and the ICP term
+  // are added by ONE of the waves that share a pixel's channels (channel-split march).
+  float cnt_w = 1.0f;
   // the seven per-pixel channel sums -> JtJ / JtR / invalid count / extremum corrections
   struct Sums {
     float Saa[R], Sab[R], Sbb[R], Sa[R], Sb[R], Sar[R], Sbr[R];
@@ -1236,8 +1243,8 @@ __global__ __launch_bounds__(kThreads, DPFT_MIN_WAVES) void ic_reduce_kernel(Ite
       }
 #pragma unroll
       for (int i = 0; i < 6; ++i) acc[21 + i] -= cA * Jx[i] + cB * Jy[i];
-      ninv += invalid ? 1.0f : 0.0f;
-      if (ICP) {  // JtWJ += (wJ)^T (wJ), JtR += (wJ)^T (w r)  (algorithms.py:668-689)
+      ninv += invalid ? cnt_w : 0.0f;
+      if (ICP && cnt_w != 0.0f) {  // JtWJ += (wJ)^T (wJ), JtR += (wJ)^T (w r)  (algorithms.py:668-689)
         const int yr = F.y0 + r;
         const float d0v = p.depth0[(size_t)b * HW + yr * W + F.xc];
         const IcpTerm ic = icp_pixel(F.wp[r].xr, F.wp[r].yr, d0v, Rm, tv, fx, fy, cx, cy, H, W,
@@ -1264,7 +1271,7 @@ __global__ __launch_bounds__(kThreads, DPFT_MIN_WAVES) void ic_reduce_kernel(Ite
           const float dB = invalid ? 0.0f : (1e-6f * Sb - Sbr);
 #pragma unroll
           for (int i = 0; i < 6; ++i) corr[i] = -(dA * Jx[i] + dB * Jy[i]);
-          corr[6] = invalid ? 0.0f : 1.0f;
+          corr[6] = invalid ? 0.0f : cnt_w;
           if (le) {
             const bool reset = sr0 < mn0;
             mn0 = sr0;
@@ -1295,10 +1302,18 @@ __global__ __launch_bounds__(kThreads, DPFT_MIN_WAVES) void ic_reduce_kernel(Ite
     constexpr int NQ = CT / 4;
     static_assert(CT % 4 == 0, "channel quads");
     const int U = p.tiles_x * H;
-    const int nw = p.nbpp * 4, jw = jb * 4 + wave;
-    const int ubeg = (int)(((long)U * jw) / nw), uend = (int)(((long)U * (jw + 1)) / nw);
+    // kMarchCSplit waves share a band, each with NQW of the NQ channel quads: the JtJ /
+    // JtR terms are linear in a pixel's channel sums, so each wave accumulates its own
+    // share with no exchange; a band row takes 1/kMarchCSplit of the time, so the f1 tap
+    // row a row shares with the next is re-requested before L2 has cycled.
+    constexpr int CSP = (NQ / kMarchCSplit >= 2) ? kMarchCSplit : (NQ >= 4 ? NQ / 2 : 1), NQW = NQ / CSP;
+    static_assert(NQ % CSP == 0 && 4 % CSP == 0, "channel split");
+    const int jw = jb * 4 + wave, band = jw / CSP, sub = jw - band * CSP, nw = p.nbpp * 4 / CSP;
+    const int qbase = sub * NQW;
+    cnt_w = sub == 0 ? 1.0f : 0.0f;
+    const int ubeg = (int)(((long)U * band) / nw), uend = (int)(((long)U * (band + 1)) / nw);
     const int nrows = uend - ubeg;
-    const bool up = (jw & 1) != 0;
+    const bool up = (band & 1) != 0;
     const int dir = up ? -1 : 1;
     const float dirf = up ? -1.0f : 1.0f;
     const int row_restart = up ? H - 1 : 0;  // a strip begins here in marching order
@@ -1336,7 +1351,7 @@ __global__ __launch_bounds__(kThreads, DPFT_MIN_WAVES) void ic_reduce_kernel(Ite
     // in slot 1, which is the window of the next step.
     auto stepn = [&](auto NSC, int k) {
       constexpr int NS = decltype(NSC)::value;
-      constexpr int NU = NQ * NS;
+      constexpr int NU = NQW * NS;
       int xs, yr[NS];
       unit_pos(k, xs, yr[0]);
       if constexpr (NS == 2) {
@@ -1349,9 +1364,10 @@ __global__ __launch_bounds__(kThreads, DPFT_MIN_WAVES) void ic_reduce_kernel(Ite
       if (k == 0 || yr[0] == row_restart) {  // prime the window: rows y - dir (replicate-clamped) and y
         const int yp = min(max(yr[0] - dir, 0), H - 1);
 #pragma unroll
-        for (int q = 0; q < NQ; ++q) {
-          win[q * 64 + lane] = llvm_buf_load_f32x4(rf0, colq, q * 4 * (int)planeB + yp * W * 16, kF0Aux);
-          win[(NQ + q) * 64 + lane] = llvm_buf_load_f32x4(rf0, colq, q * 4 * (int)planeB + yr[0] * W * 16, kF0Aux);
+        for (int q = 0; q < NQW; ++q) {
+          const int po = (qbase + q) * 4 * (int)planeB;
+          win[q * 64 + lane] = llvm_buf_load_f32x4(rf0, colq, po + yp * W * 16, kF0Aux);
+          win[(NQW + q) * 64 + lane] = llvm_buf_load_f32x4(rf0, colq, po + yr[0] * W * 16, kF0Aux);
         }
         if (CS1 && !NOSIG) {
           sprev = bld(rs0, colq >> 2, yp * W * 4);
@@ -1374,7 +1390,7 @@ __global__ __launch_bounds__(kThreads, DPFT_MIN_WAVES) void ic_reduce_kernel(Ite
 #if DPFT_ABL == 1  // profiling ablation: no channel loop (frame + epilogue only)
         return;
 #endif
-        const int po = q * 4 * (int)planeB;
+        const int po = (qbase + q) * 4 * (int)planeB;
         Qm.f = llvm_buf_load_f32x4(rf0, colq, po + yn[r] * W * 16, kF0Aux);
 #if DPFT_ABL == 3  // profiling ablation: no f1 gathers
         Qm.t[0] = Qm.t[1] = Qm.t[2] = Qm.t[3] = Qm.f;
@@ -1385,7 +1401,7 @@ __global__ __launch_bounds__(kThreads, DPFT_MIN_WAVES) void ic_reduce_kernel(Ite
         Qm.t[3] = bld4(rf1, F[r].tp[0].ob1 * 16 + 16, po);
 #endif
       };
-      static_assert(kRingM == 2 && NQ % 2 == 0, "two units in flight, whole (quad, row) groups per round");
+      static_assert(kRingM == 2 && NQW % 2 == 0, "two units in flight, whole (quad, row) groups per round");
       issue(L[0], 0, WaveIdx<0>{});
       if (CS1 && !NOSIG) {
         // sigma0 rows top / centre / bottom of each row (marching direction folded in)
@@ -1417,8 +1433,8 @@ __global__ __launch_bounds__(kThreads, DPFT_MIN_WAVES) void ic_reduce_kernel(Ite
 #if DPFT_ABL == 1
         return;
 #endif
-        f32x4* s0p = win + q * 64 + lane;         // slot 0
-        f32x4* s1p = win + (NQ + q) * 64 + lane;  // slot 1
+        f32x4* s0p = win + q * 64 + lane;          // slot 0
+        f32x4* s1p = win + (NQW + q) * 64 + lane;  // slot 1
         f32x4 wtop, wmid;  // rows above / at the pixel in marching order
         if constexpr (r == 0) {
           wtop = *s0p;
