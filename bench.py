@@ -214,19 +214,24 @@ def main():
     value = iters_total / elapsed
 
     # ---- roofline of the dominant kernel: the level-0 fused reduce (+ its in-kernel
-    # finalize), i.e. exactly the launch the solve makes, continuing from the solved
-    # pose; timed with HIP events on the stream it is launched on (the current stream).
+    # finalize), i.e. exactly the launches the solve makes at level 0 -- iterations
+    # forward, reverse, forward (DPFT_ITER_REVERSE), the group repeated -- continuing
+    # from the solved pose; timed with HIP events on the stream they are launched on
+    # (the current stream).
     Rk, tk = R.clone(), t.clone()
     solver.iterate(0, Rk, tk, first=True)
-    for _ in range(2):
-        solver.iterate(0, Rk, tk)
+    l0_group = [False, True, False]
+    for rev in l0_group:
+        solver.iterate(0, Rk, tk, reverse=rev)
+    groups = max(1, a.kernel_reps // len(l0_group))
     ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     ev0.record()
-    for _ in range(a.kernel_reps):
-        solver.iterate(0, Rk, tk)
+    for _ in range(groups):
+        for rev in l0_group:
+            solver.iterate(0, Rk, tk, reverse=rev)
     ev1.record()
     torch.cuda.synchronize()
-    kern_us = ev0.elapsed_time(ev1) / a.kernel_reps * 1e3
+    kern_us = ev0.elapsed_time(ev1) / (groups * len(l0_group)) * 1e3
     alg_bytes = solver.algorithmic_bytes(0)
     achieved = alg_bytes / (kern_us * 1e-6) / 1e9
     traffic = l0_traffic() if a.layout == "c4" and B == 8 else None

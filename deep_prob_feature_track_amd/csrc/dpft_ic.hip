@@ -116,7 +116,11 @@ constexpr long kSepFinMaxPixels = DPFT_SEPFIN_MAX_PIXELS;  // ic_reduce_kernel l
 #ifndef DPFT_MARCH_CSPLIT
 #define DPFT_MARCH_CSPLIT 1
 #endif
-constexpr int kMarchCSplit = DPFT_MARCH_CSPLIT;  // waves sharing a marching band (channel quads split)
+constexpr int kMarchCSplit = DPFT_MARCH_CSPLIT;
+#ifndef DPFT_MARCH_REVERSE
+#define DPFT_MARCH_REVERSE 1
+#endif
+constexpr bool kMarchReverse = DPFT_MARCH_REVERSE != 0;  // honour DPFT_ITER_REVERSE  // waves sharing a marching band (channel quads split)
 constexpr int kMarchRows = DPFT_MARCH_ROWS;  // rows per marching step (1, or 2: -10 % f1 traffic, +11 % VALU, 4 % slower)
 constexpr int kRingM = DPFT_RING_M;       // quads in flight on the marching path (kRingM - 1 ahead)
 #ifndef DPFT_F0_AUX
@@ -370,6 +374,7 @@ struct IterParams {
   float* rec;
   int nbpp, per_pair, row_groups, rps;  // reduce kernel schedule (see ic_reduce_kernel); rps = rows per step
   int fin_on;      // 0: records only (timing hook); 1: last workgroup finalizes
+  int reverse;     // marching path: walk every band in the opposite direction (DPFT_ITER_REVERSE)
   FinParams fin;
 };
 
@@ -1313,7 +1318,9 @@ __global__ __launch_bounds__(kThreads, DPFT_MIN_WAVES) void ic_reduce_kernel(Ite
     cnt_w = sub == 0 ? 1.0f : 0.0f;
     const int ubeg = (int)(((long)U * band) / nw), uend = (int)(((long)U * (band + 1)) / nw);
     const int nrows = uend - ubeg;
-    const bool up = (band & 1) != 0;
+    // odd iterations reverse every band: they start on the rows the previous iteration
+    // read last, which are still in the Infinity Cache
+    const bool up = ((band & 1) != 0) != (kMarchReverse && p.reverse != 0);
     const int dir = up ? -1 : 1;
     const float dirf = up ? -1.0f : 1.0f;
     const int row_restart = up ? H - 1 : 0;  // a strip begins here in marching order
@@ -2560,6 +2567,7 @@ IterParams make_params(const DpftLevelDesc& d, const DpftLevelTensors& tt, const
   p.per_pair = g.tiles_x * p.row_groups;
   p.nbpp = 0;  // set at launch from the kernel's resident capacity
   p.fin_on = 0;
+  p.reverse = 0;
   memset(&p.fin, 0, sizeof(p.fin));
   p.fin.rec = p.rec;
   p.fin.prec = reinterpret_cast<double*>(static_cast<char*>(ws) + kCtrlBytes);
@@ -2730,8 +2738,9 @@ int iterate_impl(const DpftLevelDesc* desc, const DpftLevelTensors* tt, float* R
   if (!R || !t || !ws) return fail(DPFT_E_INVALID, "null pose / workspace");
   if (ws_bytes < ws_need(*desc)) return fail(DPFT_E_WORKSPACE, "workspace %zu < %zu", ws_bytes, ws_need(*desc));
   const Geometry g = plan(*desc);
-  if (first && (rc = launch_minmax(*desc, *tt, ws, st))) return rc;
+  if ((first & DPFT_ITER_FIRST) && (rc = launch_minmax(*desc, *tt, ws, st))) return rc;
   IterParams p = make_params(*desc, *tt, g, R, t, ws);
+  p.reverse = (first & DPFT_ITER_REVERSE) ? 1 : 0;
   p.fin_on = 1;
   p.fin.R = R;
   p.fin.t = t;
@@ -2794,7 +2803,8 @@ int dpft_ic_solve_level(const DpftLevelDesc* desc, const DpftLevelTensors* tenso
   if (rc) return rc;
   for (int it = 0; it < desc->iters; ++it) {
     const bool last = it == desc->iters - 1;
-    rc = iterate_impl(desc, tensors, R, t, last ? jtj_out : nullptr, last ? jtr_out : nullptr, nullptr, it == 0,
+    const int flags = (it == 0 ? DPFT_ITER_FIRST : 0) | ((it & 1) ? DPFT_ITER_REVERSE : 0);
+    rc = iterate_impl(desc, tensors, R, t, last ? jtj_out : nullptr, last ? jtr_out : nullptr, nullptr, flags,
                       workspace, workspace_bytes, static_cast<hipStream_t>(hip_stream));
     if (rc) return rc;
   }

@@ -196,15 +196,17 @@ def solve_level(pose, x0, x1, invD0, invD1, K, sigma0, sigma1, iters=3, return_j
     return out + (jtj,) if return_jtj else out
 
 
-def iterate(pose, x0, x1, invD0, invD1, K, sigma0, sigma1, first=True, **kw):
-    """One iteration; returns (R, t [B,3,1], JtJ [B,6,6], JtR [B,6], invalid [B]) -- test / trace API."""
+def iterate(pose, x0, x1, invD0, invD1, K, sigma0, sigma1, first=True, reverse=False, **kw):
+    """One iteration; returns (R, t [B,3,1], JtJ [B,6,6], JtR [B,6], invalid [B]) -- test / trace API.
+    reverse=True: the marching order of the solve's odd iterations (DPFT_ITER_REVERSE)."""
     c = LevelCall(x0, x1, invD0, invD1, K, sigma0, sigma1, iters=1, **kw)
     R, t = c.pose_buffers(pose)
     jtj = torch.empty(c.B, 6, 6, dtype=torch.float32, device=c.device)
     jtr = torch.empty(c.B, 6, dtype=torch.float32, device=c.device)
     inv = torch.empty(c.B, dtype=torch.int32, device=c.device)
     rc = N.lib().dpft_ic_iterate(ctypes.byref(c.desc), ctypes.byref(c.tens), _ptr(R), _ptr(t), _ptr(jtj), _ptr(jtr),
-                                 _ptr(inv), int(bool(first)), _ptr(c.ws), c.ws_bytes, _stream(c.device))
+                                 _ptr(inv), (1 if first else 0) | (2 if reverse else 0), _ptr(c.ws), c.ws_bytes,
+                                 _stream(c.device))
     N.check(rc, "dpft_ic_iterate")
     return R, t.view(c.B, 3, 1), jtj, jtr, inv
 
@@ -314,14 +316,16 @@ class PyramidSolver:
                                        _ptr(self.ws), self.ws_bytes, st)
             N.check(rc, "dpft_ic_solve_level")
 
-    def iterate(self, level, R, t, first=False):
+    def iterate(self, level, R, t, first=False, reverse=False):
         """One full iteration (fused reduce + in-kernel finalize) of `level`, in place.
 
         With first=False it reuses the sigma0 extrema the last pass over this level left
-        in the workspace; bench.py times the dominant kernel this way."""
+        in the workspace; reverse=True walks the level in the order the solve uses on odd
+        iterations (DPFT_ITER_REVERSE).  bench.py times the dominant kernel this way."""
         c = self.calls[level]
+        flags = (1 if first else 0) | (2 if reverse else 0)
         rc = N.lib().dpft_ic_iterate(ctypes.byref(c.desc), ctypes.byref(c.tens), _ptr(R), _ptr(t), None, None, None,
-                                     int(first), _ptr(self.ws), self.ws_bytes, _stream(self.device))
+                                     flags, _ptr(self.ws), self.ws_bytes, _stream(self.device))
         N.check(rc, "dpft_ic_iterate")
 
     def reduce_only(self, level, R, t):

@@ -126,10 +126,16 @@ int dpft_ic_solve_level(const DpftLevelDesc* desc, const DpftLevelTensors* tenso
 
 /*
  * One iteration (residual -> Jacobian -> JtJ/JtR -> damped solve -> update).
- * `first` must be non-zero on the first iteration of a level (it computes the
- * per-level sigma0 extrema).  invalid_out [B] (nullable, int32) receives the
- * number of invalid pixels of this iteration's residual.
+ * `first`: bit 0 (DPFT_ITER_FIRST) must be set on the first iteration of a level
+ * (it computes the per-level sigma0 extrema); bit 1 (DPFT_ITER_REVERSE) walks the
+ * level in the reverse order (dpft_ic_solve_level sets it on odd iterations, so
+ * an iteration starts on the bytes the previous one read last, still in the
+ * Infinity Cache; same arithmetic, different fp32 summation grouping).
+ * invalid_out [B] (nullable, int32) receives the number of invalid pixels of
+ * this iteration's residual.
  */
+#define DPFT_ITER_FIRST 1u
+#define DPFT_ITER_REVERSE 2u
 int dpft_ic_iterate(const DpftLevelDesc* desc, const DpftLevelTensors* tensors,
                     float* R, float* t, float* jtj_out, float* jtr_out, int32_t* invalid_out,
                     int first, void* workspace, size_t workspace_bytes, void* hip_stream);

@@ -152,7 +152,14 @@ def test_c4_rejects_per_channel_sigma():
         ic.solve_level(pose, x, x, d, d, K, s, s)
 
 
-SCHEDULES = ["march", "split"]
+SCHEDULES = ["march", "march-reverse", "split"]
+
+
+def _sched_kw(schedule):
+    """test schedule name -> ic.iterate keywords ("march-reverse": the odd-iteration order)"""
+    if schedule == "march-reverse":
+        return dict(schedule="march", reverse=True)
+    return dict(schedule=schedule)
 
 
 @pytest.mark.parametrize("schedule", SCHEDULES)
@@ -174,7 +181,7 @@ def test_c4_schedules_from_reference_pose(schedule):
             R = torch.from_numpy(z["f32_R"][i - 1]).to(dev) if i else R0
             t = (torch.from_numpy(z["f32_t"][i - 1]).to(dev) if i else t0).reshape(-1, 3, 1)
             out = []
-            for (f0, f1), kw in (((d["f0"], d["f1"]), {}), (packed, dict(schedule=schedule))):
+            for (f0, f1), kw in (((d["f0"], d["f1"]), {}), (packed, _sched_kw(schedule))):
                 o = ic.iterate((R, t), f0, f1, d["invD0"], d["invD1"], K / 2 ** l, d["s0"], d["s1"], first=True,
                                remove_tru_sigma=bool(z["opt_remove_tru_sigma"]), **kw)
                 out.append([x.cpu().numpy() for x in o])
@@ -217,7 +224,7 @@ def test_c4_schedules_random(schedule, C, H, W, no_unc, masks):
     sa, sb = (None, None) if no_unc else (s0, s1)
     a = ic.iterate((R, t), f0, f1, d0, d1, K, sa, sb, first=True, **kw)
     b = ic.iterate((R, t), ic.pack_features(f0), ic.pack_features(f1), d0, d1, K, sa, sb, first=True,
-                   schedule=schedule, **kw)
+                   **_sched_kw(schedule), **kw)
     assert torch.equal(a[4], b[4])  # invalid counts
     torch.testing.assert_close(b[2], a[2], rtol=2e-6, atol=1e-6 * a[2].abs().max().item())
     torch.testing.assert_close(b[3], a[3], rtol=1e-4, atol=1e-5 * a[3].abs().max().item())

@@ -1,0 +1,29 @@
+"""Build compile-time variants of libdpft_ic.so under tools/libs/ for A/B runs on the GPU box
+(select one with DPFT_LIB=tools/libs/libdpft_<name>.so; tools/kbench.py honours it).
+
+python tools/build_variants.py name=-DFLAG=V[,-DFLAG2=V] ...
+"""
+import os
+import subprocess
+import sys
+from concurrent.futures import ThreadPoolExecutor
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+from deep_prob_feature_track_amd import build as B  # noqa: E402
+
+
+def one(spec):
+    name, flags = spec.split("=", 1)
+    out = os.path.join(ROOT, "tools", "libs", f"libdpft_{name}.so")
+    os.makedirs(os.path.dirname(out), exist_ok=True)
+    cmd = [B.HIPCC, f"--offload-arch={B.ARCH}", "-O3", "-std=c++17", "-shared", "-fPIC", f"-I{B.INC}",
+           *[f for f in flags.split(",") if f], "-o", out, B.SRC]
+    subprocess.run(cmd, check=True)
+    return out
+
+
+if __name__ == "__main__":
+    with ThreadPoolExecutor(4) as ex:
+        for o in ex.map(one, sys.argv[1:]):
+            print(o)

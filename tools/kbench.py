@@ -16,7 +16,8 @@ p = argparse.ArgumentParser()
 p.add_argument("--level", type=int, default=0)
 p.add_argument("--batch", type=int, default=8)
 p.add_argument("--reps", type=int, default=20)
-p.add_argument("--mode", choices=["reduce", "iterate"], default="reduce")
+p.add_argument("--mode", choices=["reduce", "iterate", "level"], default="reduce",
+               help="level: the solve's launches at one level (iterations forward, reverse, forward)")
 p.add_argument("--c4", action="store_true", help="channel-quad packed features")
 p.add_argument("--schedule", default=None, help="auto | march | split (channel-quad reduce kernel)")
 a = p.parse_args()
@@ -36,7 +37,12 @@ for level in ([a.level] if a.level >= 0 else range(len(solver.calls))):
                                  None, None, None, 1, ic._ptr(solver.ws), solver.ws_bytes, ic._stream(dev))
     N.check(rc, "iterate")  # leaves this level's sigma0 extrema in the workspace
     torch.cuda.synchronize()
-    run = (lambda: solver.reduce_only(level, R, t)) if a.mode == "reduce" else (lambda: solver.iterate(level, R, t))
+    def run_level():
+        for rev in (False, True, False):
+            solver.iterate(level, R, t, reverse=rev)
+    run = {"reduce": lambda: solver.reduce_only(level, R, t), "iterate": lambda: solver.iterate(level, R, t),
+           "level": run_level}[a.mode]
+    per = 3 if a.mode == "level" else 1
     for _ in range(3):
         run()
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
@@ -45,7 +51,7 @@ for level in ([a.level] if a.level >= 0 else range(len(solver.calls))):
         run()
     e1.record()
     torch.cuda.synchronize()
-    us = e0.elapsed_time(e1) / a.reps * 1e3
+    us = e0.elapsed_time(e1) / (a.reps * per) * 1e3
     gbs = solver.algorithmic_bytes(level) / (us * 1e-6) / 1e9
     print(f"{os.path.basename(os.environ.get('DPFT_LIB', 'libdpft_ic.so'))}{' c4' if a.c4 else ''}{' ' + a.schedule if a.schedule else ''} {a.mode} level {level} B={a.batch}: "
           f"{us:.1f} us/launch, {gbs:.0f} GB/s algorithmic ({gbs / 80:.1f}% of 8 TB/s)", flush=True)
