@@ -120,9 +120,29 @@ constexpr int kMarchCSplit = DPFT_MARCH_CSPLIT;
 #ifndef DPFT_MARCH_REVERSE
 #define DPFT_MARCH_REVERSE 1
 #endif
-constexpr bool kMarchReverse = DPFT_MARCH_REVERSE != 0;  // honour DPFT_ITER_REVERSE  // waves sharing a marching band (channel quads split)
+constexpr bool kMarchReverse = DPFT_MARCH_REVERSE != 0;  // honour DPFT_ITER_REVERSE
+#ifndef DPFT_MARCH_SKEW
+#define DPFT_MARCH_SKEW 10
+#endif
+constexpr int kMarchSkew = DPFT_MARCH_SKEW;  // band-size skew of the marching schedule (64ths)  // waves sharing a marching band (channel quads split)
 constexpr int kMarchRows = DPFT_MARCH_ROWS;  // rows per marching step (1, or 2: -10 % f1 traffic, +11 % VALU, 4 % slower)
 constexpr int kRingM = DPFT_RING_M;       // quads in flight on the marching path (kRingM - 1 ahead)
+#ifndef DPFT_UNROLL_Q
+#define DPFT_UNROLL_Q 1  // marching path: the quad loop straight-line (static quad indices)
+#endif
+#ifndef DPFT_RING_Q
+#define DPFT_RING_Q 3
+#endif
+constexpr int kRingQ = DPFT_RING_Q;  // straight-line marching quad loop: quads in flight
+#ifndef DPFT_LATE_TERMS
+#define DPFT_LATE_TERMS 0
+#endif
+constexpr bool kLateTerms = DPFT_LATE_TERMS != 0;  // pixel terms after the channel loop
+#ifndef DPFT_TAP_CACHE
+#define DPFT_TAP_CACHE 1
+#endif
+// marching path: keep the leading f1 tap pair of every quad in registers for the next row
+constexpr bool kTapCache = DPFT_TAP_CACHE != 0 && DPFT_UNROLL_Q != 0 && DPFT_MARCH_ROWS == 1 && DPFT_ABL == 0;
 #ifndef DPFT_F0_AUX
 #define DPFT_F0_AUX 2
 #endif
@@ -375,6 +395,7 @@ struct IterParams {
   int nbpp, per_pair, row_groups, rps;  // reduce kernel schedule (see ic_reduce_kernel); rps = rows per step
   int fin_on;      // 0: records only (timing hook); 1: last workgroup finalizes
   int reverse;     // marching path: walk every band in the opposite direction (DPFT_ITER_REVERSE)
+  int skew;        // marching path: band-size skew, 64ths (see ic_reduce_kernel)
   FinParams fin;
 };
 
@@ -714,6 +735,9 @@ __device__ void global_extrema(const float* rec, int nblocks, int imn, int imx, 
 // (algorithms.py:2035-2054, geometry.py:105-123, 163-185):
 // R <- R Exp(-w), t <- R (-Exp(-w) v) + t.
 __device__ void solve_and_update(const double* jtj_u, const double* jtr, float* Rp, float* tp) {
+#if DPFT_ABL_SOLVE == 1  // profiling ablation: no solve / update
+  return;
+#endif
   double A[6][6];
   int k = 0;
 #pragma unroll
@@ -764,7 +788,14 @@ __device__ void solve_and_update(const double* jtj_u, const double* jtr, float* 
   const double k0 = w0 / th, k1 = w1 / th, k2 = w2 / th;
   const double Kx[9] = {0.0, -k2, k1, k2, 0.0, -k0, -k1, k0, 0.0};
   double sn, cs;
+#if DPFT_ABL_SOLVE == 2  // profiling ablation: fp32 trig
+  float snf, csf;
+  sincosf((float)th, &snf, &csf);
+  sn = snf;
+  cs = csf;
+#else
   sincos(th, &sn, &cs);
+#endif
   const double cs1 = 1.0 - cs;
   double dR[9];
 #pragma unroll
@@ -1065,6 +1096,13 @@ __device__ void finalize_loss(const FinParams& q) {
 template <int CT, bool CS1, bool TRU, int MODE, bool C4>
 __global__ __launch_bounds__(kThreads, DPFT_MIN_WAVES) void ic_reduce_kernel(IterParams p) {
   constexpr bool ICP = MODE == 1, NOSIG = MODE == 2;
+#if DPFT_TAIL_PROF  // profiling build: launch timeline in ctrl words 16..28 (tools/kbench.py --tail)
+  if (threadIdx.x == 0) {
+    const uint32_t ts = (uint32_t)wall_clock64();
+    atomicMin(p.ctrl + 16, ts);
+    if (blockIdx.x < 512) st_ag(p.ctrl + 64 + 512 + xcd_remap(blockIdx.x, gridDim.x), ts);
+  }
+#endif
   static_assert(!C4 || CS1, "the channel-quad layout needs one sigma plane");
   constexpr int R = C4 ? ((kMarch && CT > 0) ? 1 : kRPL4) : (CS1 ? kRPL : 1);  // rows per lane
   constexpr float kFill = NOSIG ? 1e-3f : 1e-6f;  // weighted residual of invalid pixels
@@ -1316,7 +1354,17 @@ __global__ __launch_bounds__(kThreads, DPFT_MIN_WAVES) void ic_reduce_kernel(Ite
     const int jw = jb * 4 + wave, band = jw / CSP, sub = jw - band * CSP, nw = p.nbpp * 4 / CSP;
     const int qbase = sub * NQW;
     cnt_w = sub == 0 ? 1.0f : 0.0f;
-    const int ubeg = (int)(((long)U * band) / nw), uend = (int)(((long)U * (band + 1)) / nw);
+    // Band sizes: the first half of a pair's waves belongs to the workgroups dispatched
+    // first, which the oldest-first issue arbitration favours over the second
+    // workgroup on the same CU; equal bands leave the second half running alone
+    // (at half occupancy) for ~20 % of the launch.  Weights 64 + skew / 64 - skew.
+    auto band_start = [&](int bnd) {
+      const int h = nw >> 1, sk = nw >= 2 ? p.skew : 0;
+      const long wsum = (long)(64 + sk) * min(bnd, h) + (long)(64 - sk) * max(bnd - h, 0);
+      const long wtot = (long)(64 + sk) * h + (long)(64 - sk) * (nw - h);
+      return (int)(((long)U * wsum) / wtot);
+    };
+    const int ubeg = band_start(band), uend = band_start(band + 1);
     const int nrows = uend - ubeg;
     // odd iterations reverse every band: they start on the rows the previous iteration
     // read last, which are still in the Infinity Cache
@@ -1336,8 +1384,17 @@ __global__ __launch_bounds__(kThreads, DPFT_MIN_WAVES) void ic_reduce_kernel(Ite
     float sprev = 0.f, scur = 0.f;
     struct QuadM {
       f32x4 f;      // f0 row y + dir
-      f32x4 t[4];   // f1 taps (see gather4 / QuadLoadsR)
+      f32x4 t[4];   // f1 taps (see gather4 / QuadLoadsR); tap cache: trailing pair, leading pair
     };
+    // Tap cache (kTapCache): in marching order, the f1 tap row a pixel row shares with
+    // the next one is its LEADING row (lower row marching down, upper row marching up)
+    // and the next row's TRAILING row.  Each lane keeps its leading pair of every quad
+    // (pair base `tc_ob`) and the next row reloads its trailing pair only where the
+    // pair base differs: a hit returns exactly the bytes a load of that base would
+    // (f1 is read-only), so the cache changes no result, only the f1 re-fetch that
+    // otherwise misses the XCD's L2 one row-step later.
+    f32x4 tc[kTapCache ? NQW : 1][2];
+    int tc_ob = -1;
     // d of the next step's (up to) two rows, prefetched one step ahead
     float dnx[2] = {0.f, 0.f};
     auto load_d2 = [&](int k, float (&dd)[2]) {
@@ -1391,7 +1448,23 @@ __global__ __launch_bounds__(kThreads, DPFT_MIN_WAVES) void ic_reduce_kernel(Ite
         make_frame_xy(xs, yr[r], dv, F[r], false);
         snew[r] = (CS1 && !NOSIG) ? bld(rs0, colq >> 2, yn[r] * W * 4) : 0.f;
       }
-      QuadM L[kRingM];
+      // straight-line quad loop (one row per step): a ring of kRingQ quads, kRingQ - 1 ahead
+      constexpr bool kLine = DPFT_UNROLL_Q && NS == 1;
+      constexpr int RM = kLine ? (kRingQ < NQW ? kRingQ : NQW) : kRingM;
+      QuadM L[RM];
+      // tap cache: trailing / leading pair bases and weights of this row (NS == 1)
+      const int obT = up ? F[0].tp[0].ob1 : F[0].tp[0].ob0, obL = up ? F[0].tp[0].ob0 : F[0].tp[0].ob1;
+      const bool tc_hit = kTapCache && NS == 1 && obT == tc_ob;
+      PairWeights wq = F[0].pw[0];  // channel-unit weights of slots t[0..3]
+      if constexpr (kTapCache && NS == 1) {
+        tc_ob = obL;
+        if (up) {  // slots 0/1 hold the trailing pair: the lower row when marching up
+          wq.w0 = F[0].pw[0].w2;
+          wq.w1 = F[0].pw[0].w3;
+          wq.w2 = F[0].pw[0].w0;
+          wq.w3 = F[0].pw[0].w1;
+        }
+      }
       auto issue = [&](QuadM& Qm, int q, auto RC) {
         constexpr int r = decltype(RC)::value;
 #if DPFT_ABL == 1  // profiling ablation: no channel loop (frame + epilogue only)
@@ -1402,14 +1475,28 @@ __global__ __launch_bounds__(kThreads, DPFT_MIN_WAVES) void ic_reduce_kernel(Ite
 #if DPFT_ABL == 3  // profiling ablation: no f1 gathers
         Qm.t[0] = Qm.t[1] = Qm.t[2] = Qm.t[3] = Qm.f;
 #else
-        Qm.t[0] = bld4(rf1, F[r].tp[0].ob0 * 16, po);
-        Qm.t[1] = bld4(rf1, F[r].tp[0].ob0 * 16 + 16, po);
-        Qm.t[2] = bld4(rf1, F[r].tp[0].ob1 * 16, po);
-        Qm.t[3] = bld4(rf1, F[r].tp[0].ob1 * 16 + 16, po);
+        if constexpr (kTapCache && NS == 1) {
+          // branch-free: a hit lane re-requests its leading pair (an L1 hit next to the
+          // leading loads below) and selects the cached bytes; a divergent branch around
+          // the loads would make the waitcnt bookkeeping wait on the next quad's loads
+          // (the select happens at use, in unitc: here it would wait on the load at once)
+          const int offT = (tc_hit ? obL : obT) * 16;
+          Qm.t[0] = bld4(rf1, offT, po);
+          Qm.t[1] = bld4(rf1, offT + 16, po);
+          Qm.t[2] = bld4(rf1, obL * 16, po);
+          Qm.t[3] = bld4(rf1, obL * 16 + 16, po);
+        } else {
+          Qm.t[0] = bld4(rf1, F[r].tp[0].ob0 * 16, po);
+          Qm.t[1] = bld4(rf1, F[r].tp[0].ob0 * 16 + 16, po);
+          Qm.t[2] = bld4(rf1, F[r].tp[0].ob1 * 16, po);
+          Qm.t[3] = bld4(rf1, F[r].tp[0].ob1 * 16 + 16, po);
+        }
 #endif
       };
-      static_assert(kRingM == 2 && NQW % 2 == 0, "two units in flight, whole (quad, row) groups per round");
-      issue(L[0], 0, WaveIdx<0>{});
+      static_assert(kLine || (kRingM == 2 && NQW % 2 == 0), "two units in flight, whole (quad, row) groups per round");
+      static_assert(!kLine || (RM >= 2 && RM <= NQW), "ring depth");
+#pragma unroll
+      for (int i = 0; i < (kLine ? RM - 1 : 1); ++i) issue(L[i], i, WaveIdx<0>{});
       if (CS1 && !NOSIG) {
         // sigma0 rows top / centre / bottom of each row (marching direction folded in)
         const float s1n = snew[0], s2n = snew[NS - 1];
@@ -1427,9 +1514,14 @@ __global__ __launch_bounds__(kThreads, DPFT_MIN_WAVES) void ic_reduce_kernel(Ite
           scur = s1n;
         }
       }
+      // The occlusion / sigma terms only enter the epilogue (the channel sums are
+      // weight-free), so on the straight-line path they are resolved after the channel
+      // loop: the frame's depth / sigma1 gathers land behind it instead of stalling here.
       PixelTerms T[NS];
+      if constexpr (!(kLine && kLateTerms)) {
 #pragma unroll
-      for (int r = 0; r < NS; ++r) pixel_terms(F[r], T[r]);
+        for (int r = 0; r < NS; ++r) pixel_terms(F[r], T[r]);
+      }
       f32x2 Q[NS][9];
 #pragma unroll
       for (int r = 0; r < NS; ++r)
@@ -1457,7 +1549,12 @@ __global__ __launch_bounds__(kThreads, DPFT_MIN_WAVES) void ic_reduce_kernel(Ite
           Q[r][1] += f32x2{z.z, z.w};
         }
 #else
-        const PairWeights& w = F[r].pw[0];
+        const PairWeights& w = (kTapCache && NS == 1) ? wq : F[r].pw[0];
+        f32x4 tt0 = cur.t[0], tt1 = cur.t[1];  // trailing pair (cached bytes on a hit)
+        if constexpr (kTapCache && NS == 1) {
+          tt0 = tc_hit ? tc[q][0] : tt0;
+          tt1 = tc_hit ? tc[q][1] : tt1;
+        }
 #pragma unroll
         for (int h = 0; h < 2; ++h) {  // channels 4q + 2h, 4q + 2h + 1
           auto half = [&](const f32x4& v) { return h ? f32x2{v.z, v.w} : f32x2{v.x, v.y}; };
@@ -1470,7 +1567,7 @@ __global__ __launch_bounds__(kThreads, DPFT_MIN_WAVES) void ic_reduce_kernel(Ite
           const f32x2 n2 = x * x + yv * yv + 1e-8f;
           const f32x2 inv = f32x2{__builtin_amdgcn_rsqf(n2.x), __builtin_amdgcn_rsqf(n2.y)};
           const f32x2 gx = x * inv, gy = yv * inv;
-          const f32x2 res = (half(cur.t[0]) * w.w0 + half(cur.t[1]) * w.w1 + half(cur.t[2]) * w.w2 +
+          const f32x2 res = (half(tt0) * w.w0 + half(tt1) * w.w1 + half(cur.t[2]) * w.w2 +
                              half(cur.t[3]) * w.w3) - fm;
           Q[r][0] += gx * gx;
           Q[r][1] += gx * gy;
@@ -1483,6 +1580,16 @@ __global__ __launch_bounds__(kThreads, DPFT_MIN_WAVES) void ic_reduce_kernel(Ite
           Q[r][8] += res;
         }
 #endif
+        if constexpr (kTapCache && NS == 1) {  // the leading pair is the next row's trailing pair
+          tc[q][0] = cur.t[2];
+          tc[q][1] = cur.t[3];
+        }
+#if DPFT_UNROLL_Q
+        // straight-line code: the accumulators are pure arithmetic, which the DAG scheduler
+        // would otherwise sink below every later load (all quads' loads first: 400 VGPRs)
+        asm volatile("" : "+v"(Q[r][0]), "+v"(Q[r][1]), "+v"(Q[r][2]), "+v"(Q[r][3]), "+v"(Q[r][4]),
+                     "+v"(Q[r][5]), "+v"(Q[r][6]), "+v"(Q[r][7]), "+v"(Q[r][8])::"memory");
+#endif
         if constexpr (NS == 1) {  // window (y, y + dir)
           *s0p = wmid;
           *s1p = cur.f;
@@ -1492,18 +1599,32 @@ __global__ __launch_bounds__(kThreads, DPFT_MIN_WAVES) void ic_reduce_kernel(Ite
           *s1p = cur.f;
         }
       };
-      // every ring round but the last refills unconditionally: each load set keeps its registers
-      constexpr int r1 = 1 % NS;  // row of the odd units
+      if constexpr (kLine) {
+        // static quad indices (the tap cache lives in registers); each unit's accumulators
+        // are pinned at its end (unitc), so the rounds keep this order
+#pragma unroll
+        for (int qq = 0; qq < NQW; ++qq) {
+          if (qq + RM - 1 < NQW) issue(L[(qq + RM - 1) % RM], qq + RM - 1, WaveIdx<0>{});
+          unitc(qq, L[qq % RM], WaveIdx<0>{});
+        }
+      } else {
+        // every ring round but the last refills unconditionally: each load set keeps its registers
+        constexpr int r1 = 1 % NS;  // row of the odd units
 #pragma unroll 1
-      for (int u0 = 0; u0 < NU - 2; u0 += 2) {
-        issue(L[1], (u0 + 1) / NS, WaveIdx<r1>{});
-        unitc(u0 / NS, L[0], WaveIdx<0>{});
-        issue(L[0], (u0 + 2) / NS, WaveIdx<0>{});
-        unitc((u0 + 1) / NS, L[1], WaveIdx<r1>{});
+        for (int u0 = 0; u0 < NU - 2; u0 += 2) {
+          issue(L[1], (u0 + 1) / NS, WaveIdx<r1>{});
+          unitc(u0 / NS, L[0], WaveIdx<0>{});
+          issue(L[0], (u0 + 2) / NS, WaveIdx<0>{});
+          unitc((u0 + 1) / NS, L[1], WaveIdx<r1>{});
+        }
+        issue(L[1], (NU - 1) / NS, WaveIdx<r1>{});
+        unitc((NU - 2) / NS, L[0], WaveIdx<0>{});
+        unitc((NU - 1) / NS, L[1], WaveIdx<r1>{});
       }
-      issue(L[1], (NU - 1) / NS, WaveIdx<r1>{});
-      unitc((NU - 2) / NS, L[0], WaveIdx<0>{});
-      unitc((NU - 1) / NS, L[1], WaveIdx<r1>{});
+      if constexpr (kLine && kLateTerms) {
+#pragma unroll
+        for (int r = 0; r < NS; ++r) pixel_terms(F[r], T[r]);
+      }
 #pragma unroll
       for (int r = 0; r < NS; ++r) {
         Sums S;
@@ -1817,9 +1938,34 @@ __global__ __launch_bounds__(kThreads, DPFT_MIN_WAVES) void ic_reduce_kernel(Ite
     for (int k = 0; k < 6; ++k) st_ag(out + R_CMX + k, (float)(e.c[k]));
   }
   // the last workgroup of a pair reduces its records; the one completing the batch solves
+#if DPFT_TAIL_PROF
+  if (threadIdx.x == 0) {
+    const uint32_t tm = (uint32_t)wall_clock64();
+    atomicMin(p.ctrl + 17, tm);
+    atomicMax(p.ctrl + 18, tm);
+    if (kb < 1024) st_ag(p.ctrl + 64 + kb, tm);  // per-workgroup finish (minmax partial area)
+  }
+#endif
   if (p.fin_on && block_is_last(p.fin.pair_cnt + b, 1u, (uint32_t)p.nbpp)) {
     pair_reduce(p.fin, b);
-    if (block_is_last(p.fin.done_cnt, 1u, (uint32_t)p.B)) finalize_batch(p.fin);
+    if (block_is_last(p.fin.done_cnt, 1u, (uint32_t)p.B)) {
+#if DPFT_TAIL_PROF
+      const uint32_t t19 = (uint32_t)wall_clock64();
+#endif
+      finalize_batch(p.fin);
+#if DPFT_TAIL_PROF
+      __syncthreads();
+      if (threadIdx.x == 0) {
+        const uint32_t t20 = (uint32_t)wall_clock64();
+        for (int i = 0; i < 3; ++i) st_ag(p.ctrl + 24 + i, ld_ag(p.ctrl + 16 + i));
+        st_ag(p.ctrl + 27, t19);
+        st_ag(p.ctrl + 28, t20);
+        st_ag(p.ctrl + 16, 0xFFFFFFFFu);
+        st_ag(p.ctrl + 17, 0xFFFFFFFFu);
+        st_ag(p.ctrl + 18, 0u);
+      }
+#endif
+    }
   }
 }
 
@@ -1963,6 +2109,9 @@ struct SplitAcc {
 
 // Stand-alone finalize (one workgroup per pair): pair records, then the batch solve.
 __global__ __launch_bounds__(kThreads) void finalize_kernel(FinParams q) {
+#if DPFT_ABL_SOLVE == 3  // profiling ablation: empty finalize launch
+  return;
+#endif
   pair_reduce(q, blockIdx.x);
   if (block_is_last(q.done_cnt, 1u, (uint32_t)q.B)) finalize_batch(q);
 }
@@ -2568,6 +2717,8 @@ IterParams make_params(const DpftLevelDesc& d, const DpftLevelTensors& tt, const
   p.nbpp = 0;  // set at launch from the kernel's resident capacity
   p.fin_on = 0;
   p.reverse = 0;
+  p.skew = kMarchSkew;
+  if (const char* e = getenv("DPFT_DEBUG_SKEW")) p.skew = atoi(e);  // tuning only
   memset(&p.fin, 0, sizeof(p.fin));
   p.fin.rec = p.rec;
   p.fin.prec = reinterpret_cast<double*>(static_cast<char*>(ws) + kCtrlBytes);
@@ -2630,7 +2781,9 @@ int resident_blocks(const void* kernel, int threads = kThreads) {
   if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kernel, threads, 0) != hipSuccess ||
       hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
     return 0;
-  const int n = std::max(1, std::min(per_cu * cus, kMaxGrid));
+  int n = std::max(1, std::min(per_cu * cus, kMaxGrid));
+  if (const char* e = getenv("DPFT_DEBUG_GRID_CAP"))  // tuning / profiling only
+    n = std::max(1, std::min(atoi(e), kMaxGrid));
   cache.push_back({kernel, dev, n});
   return n;
 }

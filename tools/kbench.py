@@ -20,6 +20,7 @@ p.add_argument("--mode", choices=["reduce", "iterate", "level"], default="reduce
                help="level: the solve's launches at one level (iterations forward, reverse, forward)")
 p.add_argument("--c4", action="store_true", help="channel-quad packed features")
 p.add_argument("--schedule", default=None, help="auto | march | split (channel-quad reduce kernel)")
+p.add_argument("--tail", action="store_true", help="print the launch timeline of a DPFT_TAIL_PROF build")
 a = p.parse_args()
 dev = torch.device("cuda:0")
 sel, levels, K = bench.make_inputs(a.batch, 0, dev)
@@ -53,5 +54,23 @@ for level in ([a.level] if a.level >= 0 else range(len(solver.calls))):
     torch.cuda.synchronize()
     us = e0.elapsed_time(e1) / (a.reps * per) * 1e3
     gbs = solver.algorithmic_bytes(level) / (us * 1e-6) / 1e9
+    if a.tail:
+        w = solver.ws[:29 * 4].view(torch.int32).cpu().numpy().astype("int64") & 0xFFFFFFFF
+        t0 = w[24]
+        print("  tail (us from first WG start): first WG done %.1f, last WG done %.1f, pairs reduced %.1f, "
+              "batch solved %.1f" % tuple((w[i] - t0) / 100.0 for i in (25, 26, 27, 28)))
+        nb = int(c.desc.B)
+        g = int(os.environ.get("DPFT_TAIL_GRID", "512"))
+        import numpy as np
+        f = (solver.ws[:(64 + g) * 4].view(torch.int32).cpu().numpy().astype("int64")[64:] & 0xFFFFFFFF)
+        f = (f - t0) / 100.0
+        st = (solver.ws[:(64 + 512 + g) * 4].view(torch.int32).cpu().numpy().astype("int64")[64 + 512:] & 0xFFFFFFFF)
+        np.save(os.path.join(ROOT, "gpurun_out", f"tails_l{level}_{a.mode}.npy"), (st - t0) / 100.0)
+        import numpy as np
+        np.save(os.path.join(ROOT, "gpurun_out", f"tail_l{level}_{a.mode}.npy"), f)
+        per = g // nb
+        for b in range(nb):
+            x = f[b * per:(b + 1) * per]
+            print("   pair %d: finish min %.1f  median %.1f  max %.1f" % (b, x.min(), np.median(x), x.max()))
     print(f"{os.path.basename(os.environ.get('DPFT_LIB', 'libdpft_ic.so'))}{' c4' if a.c4 else ''}{' ' + a.schedule if a.schedule else ''} {a.mode} level {level} B={a.batch}: "
           f"{us:.1f} us/launch, {gbs:.0f} GB/s algorithmic ({gbs / 80:.1f}% of 8 TB/s)", flush=True)
