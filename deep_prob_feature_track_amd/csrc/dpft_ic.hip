@@ -1560,15 +1560,17 @@ __global__ __launch_bounds__(kThreads, DPFT_MIN_WAVES) void ic_reduce_kernel(Ite
           auto half = [&](const f32x4& v) { return h ? f32x2{v.z, v.w} : f32x2{v.x, v.y}; };
           const f32x2 fp = half(wtop), fm = half(wmid), fn = half(cur.f);
           const f32x2 V = (fp + fn) + 2.0f * fm;
-          const f32x2 D = (fn - fp) * dirf;  // bottom - top
+          // D in marching order: gy carries the sign dirf, folded into the odd sums
+          // (gx gy, gy res, gy) once per row below
+          const f32x2 D = fn - fp;
           const f32x2 x = f32x2{lane_from_right(V.x) - lane_from_left(V.x), lane_from_right(V.y) - lane_from_left(V.y)};
           const f32x2 yv =
               f32x2{lane_from_left(D.x) + lane_from_right(D.x), lane_from_left(D.y) + lane_from_right(D.y)} + 2.0f * D;
-          const f32x2 n2 = x * x + yv * yv + 1e-8f;
+          const f32x2 n2 = x * x + (yv * yv + 1e-8f);
           const f32x2 inv = f32x2{__builtin_amdgcn_rsqf(n2.x), __builtin_amdgcn_rsqf(n2.y)};
           const f32x2 gx = x * inv, gy = yv * inv;
-          const f32x2 res = (half(tt0) * w.w0 + half(tt1) * w.w1 + half(cur.t[2]) * w.w2 +
-                             half(cur.t[3]) * w.w3) - fm;
+          const f32x2 res = ((half(tt0) * w.w0 - fm) + half(tt1) * w.w1) + half(cur.t[2]) * w.w2 +
+                            half(cur.t[3]) * w.w3;
           Q[r][0] += gx * gx;
           Q[r][1] += gx * gy;
           Q[r][2] += gy * gy;
@@ -1631,6 +1633,9 @@ __global__ __launch_bounds__(kThreads, DPFT_MIN_WAVES) void ic_reduce_kernel(Ite
         float q[9];
 #pragma unroll
         for (int i = 0; i < 9; ++i) q[i] = Q[r][i].x + Q[r][i].y;
+        q[1] *= dirf;  // gy was accumulated in marching order
+        q[4] *= dirf;
+        q[7] *= dirf;
         const float A = T[r].inv_s[0], bx = T[r].kk[0] * T[r].hx[0], by = T[r].kk[0] * T[r].hy[0], A2 = A * A;
         S.Saa[0] = A2 * q[0] + 2.0f * A * bx * q[3] + bx * bx * q[5];
         S.Sab[0] = A2 * q[1] + A * by * q[3] + A * bx * q[4] + bx * by * q[5];
