@@ -84,6 +84,49 @@ def l0_traffic():
     return None
 
 
+def copy_peak_gbs(device, nbytes=1 << 30, reps=5):
+    """Measured HBM copy rate (torch's copy kernel, read + write bytes / time): the
+    practical ceiling SURVEY.md 8(d) asks the roofline to be reported against too."""
+    x = torch.empty(nbytes // 4, dtype=torch.float32, device=device)
+    y = torch.empty_like(x)
+    x.fill_(1.0)
+    for _ in range(2):
+        y.copy_(x)
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    for _ in range(reps):
+        y.copy_(x)
+    e1.record()
+    torch.cuda.synchronize()
+    gbs = 2 * nbytes * reps / (e0.elapsed_time(e1) * 1e-3) / 1e9
+    del x, y
+    return gbs
+
+
+def cpu_model():
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return "unknown"
+
+
+def cpu_solve_seconds(lv, Kc, threads):
+    """One oracle solve of one pair on `threads` host threads (no warm-up)."""
+    from oracle import ic_oracle as O
+    old = torch.get_num_threads()
+    torch.set_num_threads(threads)
+    try:
+        with torch.no_grad():
+            t_start = time.perf_counter()
+            O.solve_pyramid(torch.eye(3)[None], torch.zeros(1, 3, 1), lv, Kc, iters=ITERS, remove_tru_sigma=True)
+            return time.perf_counter() - t_start
+    finally:
+        torch.set_num_threads(old)
+
+
 def cpu_baseline(levels_gpu, K, R_gpu, t_gpu):
     """Oracle (PyTorch-CPU restatement of the reference solver) on pair 0: 1 warm-up, best of 2."""
     from oracle import ic_oracle as O
@@ -101,6 +144,7 @@ def cpu_baseline(levels_gpu, K, R_gpu, t_gpu):
             el = time.perf_counter() - t_start
             if rep > 0:
                 best = min(best, el)
+    one_thread = cpu_solve_seconds(lv, Kc, 1)
     Ro, to = out
     dR = (R_gpu[:1].cpu() - Ro).abs().max().item()
     dt = (t_gpu[:1].cpu().view(1, 3) - to.view(1, 3)).abs().max().item()
@@ -109,7 +153,7 @@ def cpu_baseline(levels_gpu, K, R_gpu, t_gpu):
     d0 = 1.0 / lv[0]["invD0"].clamp(min=1e-6)
     epe = epe3d_between(R_gpu[:1].cpu(), t_gpu[:1].cpu().view(1, 3), Ro, to.view(1, 3), d0,
                         Kc, invalid=(lv[0]["invD0"] <= 0)).item()
-    return best, dR, dt, epe
+    return best, dR, dt, epe, one_thread
 
 
 def main():
@@ -123,6 +167,9 @@ def main():
         dist.init_process_group("nccl")
     device = torch.device("cuda", local)
     torch.cuda.set_device(device)
+    if os.environ.get("DPFT_LIB"):  # A/B runs of compile-time variants (tools/build_variants.py)
+        from deep_prob_feature_track_amd import _native
+        _native.LIB_PATH = os.path.abspath(os.environ["DPFT_LIB"])
     from deep_prob_feature_track_amd import ic, shard
 
     B = a.batch_per_gpu
@@ -235,6 +282,7 @@ def main():
     alg_bytes = solver.algorithmic_bytes(0)
     achieved = alg_bytes / (kern_us * 1e-6) / 1e9
     traffic = l0_traffic() if a.layout == "c4" and B == 8 else None
+    copy_gbs = copy_peak_gbs(device) if rank == 0 else None
 
     # secondary (rank 0 only, not the headline): the same solve from the other resident
     # layout, and the one-time cost of packing NCHW pyramids into the channel-quad layout
@@ -258,9 +306,10 @@ def main():
 
     cpu = None
     if rank == 0 and world == 1 and not a.no_cpu_baseline:
-        best, dR, dt, epe = cpu_baseline(levels_nchw, K, R, t)
+        best, dR, dt, epe, one_thread = cpu_baseline(levels_nchw, K, R, t)
         cpu = {"value": LEVELS * ITERS / best, "unit": "IC iterations/s",
-               "cores": torch.get_num_threads(), "kind": "port",
+               "cores": torch.get_num_threads(), "kind": "port", "cpu_model": cpu_model(),
+               "value_1_thread": LEVELS * ITERS / one_thread, "seconds_per_pair_1_thread": one_thread,
                "sample": "1 pair, 640x480 C=32, 4 levels x 3 iters, oracle/ic_oracle.py (PyTorch-CPU fp32 "
                          "restatement of algorithms.py:611-723), best of 2 after 1 warm-up",
                "seconds_per_pair": best, "gpu_vs_oracle_max_abs_dR": dR, "gpu_vs_oracle_max_abs_dt": dt,
@@ -284,7 +333,9 @@ def main():
                          "traffic": traffic["hbm_bytes"] if traffic else None,
                          "traffic_source": traffic["source"] if traffic else None,
                          "kernel": f"ic_reduce_kernel<32,Cs=1,tru,U_IC,{a.layout}> (level 0, + in-kernel finalize)",
-                         "kernel_us": kern_us, "algorithmic_bytes_per_launch": alg_bytes},
+                         "kernel_us": kern_us, "algorithmic_bytes_per_launch": alg_bytes,
+                         "measured_copy_peak": copy_gbs,
+                         "frac_of_measured_copy_peak": achieved / copy_gbs if copy_gbs else None},
             "cpu_baseline": cpu,
             "other_layout": other,
         }

@@ -178,6 +178,16 @@ constexpr int L_SUM = 0, L_NINV = 1, L_MN_ALL = 2, L_MN0 = 3, L_LMN = 4, L_NMN =
 constexpr int kCtlMin = 0, kCtlMax = 1, kCtlDone = 2, kCtlMMDone = 3, kCtlResDone = 4, kCtlD1Min = 8,
               kCtlPart = 64, kCtlPair = 1152;
 constexpr int kMaxMMBlocks = 512;
+#ifndef DPFT_MM_GRID
+#define DPFT_MM_GRID 128
+#endif
+#ifndef DPFT_MM_LOADS
+#define DPFT_MM_LOADS 8
+#endif
+// minmax_kernel: workgroups (<= kMaxMMBlocks) and 16-byte loads in flight per thread.
+// Its last-workgroup reduction serialises one counter arrival per workgroup.
+constexpr int kMMGrid = DPFT_MM_GRID, kMMLoads = DPFT_MM_LOADS;
+static_assert(kMMGrid <= kMaxMMBlocks, "minmax partials");
 constexpr int kMaxPairs = 2048;  // per call (one completion counter per pair)
 constexpr int kMaxGrid = 4096;   // reduce-kernel workgroups (resident capacity is far below)
 constexpr size_t kCtrlBytes = 16384;
@@ -2464,12 +2474,12 @@ __global__ __launch_bounds__(kThreads) void minmax_kernel(const float* __restric
   const size_t stride = (size_t)gridDim.x * kThreads;
   const size_t t0 = (size_t)blockIdx.x * kThreads + threadIdx.x;
   size_t i = t0;
-  for (; i + 3 * stride < n4; i += 4 * stride) {
-    f32x4 v[4];
+  for (; i + (kMMLoads - 1) * stride < n4; i += kMMLoads * stride) {
+    f32x4 v[kMMLoads];
 #pragma unroll
-    for (int u = 0; u < 4; ++u) v[u] = __builtin_nontemporal_load(s4 + i + u * stride);
+    for (int u = 0; u < kMMLoads; ++u) v[u] = __builtin_nontemporal_load(s4 + i + u * stride);
 #pragma unroll
-    for (int u = 0; u < 4; ++u) {
+    for (int u = 0; u < kMMLoads; ++u) {
       mn = fminf(mn, fminf(fminf(v[u].x, v[u].y), fminf(v[u].z, v[u].w)));
       mx = fmaxf(mx, fmaxf(fmaxf(v[u].x, v[u].y), fmaxf(v[u].z, v[u].w)));
     }
@@ -2745,7 +2755,7 @@ int hip_check(const char* what) {
 }
 
 int minmax_into(const float* src, size_t n, uint32_t* ctrl, int slot, hipStream_t st) {
-  const int grid = (int)std::min<size_t>((n + kThreads * 16 - 1) / (kThreads * 16), kMaxMMBlocks);
+  const int grid = (int)std::min<size_t>((n + kThreads * 4 * kMMLoads - 1) / (kThreads * 4 * kMMLoads), kMMGrid);
   hipLaunchKernelGGL(minmax_kernel, dim3(grid), dim3(kThreads), 0, st, src, n, ctrl, slot);
   return hip_check("minmax_kernel");
 }
