@@ -2755,7 +2755,7 @@ int hip_check(const char* what) {
 }
 
 int minmax_into(const float* src, size_t n, uint32_t* ctrl, int slot, hipStream_t st) {
-  const int grid = (int)std::min<size_t>((n + kThreads * 4 * kMMLoads - 1) / (kThreads * 4 * kMMLoads), kMMGrid);
+  const int grid = (int)std::min<size_t>((n + kThreads * 16 - 1) / (kThreads * 16), kMMGrid);
   hipLaunchKernelGGL(minmax_kernel, dim3(grid), dim3(kThreads), 0, st, src, n, ctrl, slot);
   return hip_check("minmax_kernel");
 }

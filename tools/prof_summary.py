@@ -5,7 +5,7 @@ usage: python tools/prof_summary.py --trace DIR/bench_kernel_trace.csv \
            [--traffic profiles/r1_l0_traffic.json] --out profiles/r1_summary [--title T]
 
 Every launch is assigned to a pyramid level by the sigma0 min/max pass that opens the
-level (its grid is the level's size: smallest = level 3), and to the feature layout
+level (the smallest grid opens level 3, each later pass the next finer level), and to the feature layout
 (channel-quad kernels carry `true>` / are the split kernel; the NCHW comparison solve
 `false>`).  Writes <out>.md and <out>.json: per (layout, level, kernel) the number of
 launches and their average / min / max duration, and one solve's timeline.
@@ -32,7 +32,7 @@ def main():
     a = ap.parse_args()
     rows = sorted(csv.DictReader(open(a.trace)), key=lambda r: int(r["Start_Timestamp"]))
     mm_grids = sorted({int(r["Grid_Size_X"]) for r in rows if "minmax" in r["Kernel_Name"]})
-    level_of_grid = {g: len(mm_grids) - 1 - i for i, g in enumerate(mm_grids)}
+    top = 3  # coarsest level of the 4-level bench pyramid
     groups = collections.defaultdict(list)
     level = None
     timeline, cur, solves = [], [], []
@@ -40,8 +40,13 @@ def main():
         name = short(r["Kernel_Name"])
         dur = (int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e3
         if "minmax" in name:
-            level = level_of_grid[int(r["Grid_Size_X"])]
-            if level == len(mm_grids) - 1 and cur:
+            # the smallest sigma0 pass opens level 3; each later one opens the next finer
+            # level (levels 2..0 may share a capped grid)
+            if int(r["Grid_Size_X"]) == mm_grids[0]:
+                level = top
+            else:
+                level = max((level if level is not None else top) - 1, 0)
+            if level == top and cur:
                 solves.append(cur)
                 cur = []
         if level is None:
