@@ -226,12 +226,24 @@ def main():
         return solver, R, t, run, graph is not None
 
     solver, R, t, run, graphed = make_step(levels)
-    gathered = torch.empty(world * B, 12, device=device) if world > 1 else None
+    # N > 1: the pose gather of step k runs on the collective stream while step k + 1
+    # solves (double-buffered output; poses packed into a fresh buffer first); every
+    # gather is waited for inside the timed region (drain())
+    gathered = [torch.empty(world * B, 12, device=device) for _ in range(2)] if world > 1 else None
+    pending = [None]
+    nstep = [0]
+
+    def drain():
+        if pending[0] is not None:
+            pending[0].wait()
+            pending[0] = None
 
     def step():
         run()
         if world > 1:
-            shard.gather_poses(R, t, out=gathered)
+            drain()
+            _, pending[0] = shard.gather_poses(R, t, out=gathered[nstep[0] % 2], async_op=True)
+            nstep[0] += 1
 
     def barrier():
         if world > 1:
@@ -240,12 +252,14 @@ def main():
 
     for _ in range(a.warmup):
         step()
+    drain()
     torch.cuda.synchronize()
     barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for _ in range(a.steps):
         step()
+    drain()
     torch.cuda.synchronize()
     barrier()
     torch.cuda.synchronize()

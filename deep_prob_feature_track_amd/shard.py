@@ -29,18 +29,21 @@ def unpack_poses(P):
     return P[:, :9].reshape(-1, 3, 3), P[:, 9:].reshape(-1, 3, 1)
 
 
-def gather_poses(R, t, out=None):
+def gather_poses(R, t, out=None, async_op=False):
     """All-gather every rank's [B,12] poses into [world*B, 12] (rank-major).
 
     Equal shard sizes on every rank (the bench's weak-scaling layout).  RCCL uses
     the single-buffer all_gather_into_tensor; other backends (gloo in the CPU
-    tests) the list form."""
+    tests) the list form.  The poses are packed into a fresh buffer first, so with
+    async_op=True the caller may overwrite R / t at once (the next solve) while the
+    gather runs on the collective stream; it returns (out, work) and `out` is valid
+    after work.wait()."""
     P = pack_poses(R, t)
     world = dist.get_world_size()
     if out is None:
         out = torch.empty(world * P.shape[0], 12, dtype=P.dtype, device=P.device)
     if dist.get_backend() == "nccl":
-        dist.all_gather_into_tensor(out, P)
+        work = dist.all_gather_into_tensor(out, P, async_op=async_op)
     else:
-        dist.all_gather(list(out.chunk(world, 0)), P)
-    return out
+        work = dist.all_gather(list(out.chunk(world, 0)), P, async_op=async_op)
+    return (out, work) if async_op else out

@@ -61,8 +61,14 @@ def _worker(rank, world, port, q, paths):
         b, e = shard.shard_range(len(PAIRS), world, rank)
         R, t = _solve_pairs(PAIRS[b:e])
         out = shard.gather_poses(R, t)
+        # bench.py's pipelined form: async gather, poses overwritten at once (next solve)
+        out2, work = shard.gather_poses(R, t, async_op=True)
+        R.zero_()
+        t.zero_()
+        work.wait()
         if rank == 0:
             q.put(out.clone())
+            q.put(out2.clone())
     finally:
         dist.destroy_process_group()
 
@@ -83,6 +89,7 @@ def test_two_rank_gloo_gather_matches_per_shard_solves():
     for p in procs:
         p.start()
     gathered = q.get(timeout=120)
+    gathered_async = q.get(timeout=120)
     for p in procs:
         p.join(timeout=60)
         assert p.exitcode == 0
@@ -91,3 +98,4 @@ def test_two_rank_gloo_gather_matches_per_shard_solves():
         b, e = shard.shard_range(len(PAIRS), world, r)
         expect.append(shard.pack_poses(*_solve_pairs(PAIRS[b:e])))
     assert torch.equal(gathered, torch.cat(expect, 0))
+    assert torch.equal(gathered_async, gathered)
