@@ -45,7 +45,7 @@ def _trace(name, dev, pack):
     return case, z, out
 
 
-@pytest.mark.parametrize("B,C,H,W", [(2, 8, 37, 70), (1, 32, 120, 160), (3, 4, 5, 3)])
+@pytest.mark.parametrize("B,C,H,W", [(2, 8, 37, 70), (1, 32, 120, 160), (3, 4, 5, 3), (2, 16, 6, 10), (8, 32, 60, 80)])
 def test_pack_round_trip_bit_exact(B, C, H, W):
     from deep_prob_feature_track_amd import ic
     dev = _dev()
