@@ -161,10 +161,14 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    # rehearsal knobs (tests of the N > 1 logic on a 1-GPU box): DPFT_BENCH_BACKEND=gloo
+    # and DPFT_BENCH_SHARE_GPU=1 put every rank on cuda:0; the driver's runs use neither
+    if os.environ.get("DPFT_BENCH_SHARE_GPU"):
+        local = 0
     if world > 1:
         import torch.distributed as dist
         torch.cuda.set_device(local)
-        dist.init_process_group("nccl")
+        dist.init_process_group(os.environ.get("DPFT_BENCH_BACKEND", "nccl"))
     device = torch.device("cuda", local)
     torch.cuda.set_device(device)
     if os.environ.get("DPFT_LIB"):  # A/B runs of compile-time variants (tools/build_variants.py)
