@@ -198,7 +198,8 @@ def main():
     pose_init = torch.cat((torch.eye(3, device=device).repeat(B, 1, 1).reshape(-1), torch.zeros(B * 3, device=device)))
 
     def make_step(levels):
-        solver = ic.PyramidSolver(levels, K, iters=ITERS, remove_tru_sigma=True)
+        solver = ic.PyramidSolver(levels, K, iters=ITERS, remove_tru_sigma=True,
+                                  schedule=os.environ.get("DPFT_BENCH_SCHEDULE"))  # A/B only
         pose = pose_init.clone()
         R, t = pose[:9 * B].view(B, 3, 3), pose[9 * B:].view(B, 3)
 
