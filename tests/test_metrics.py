@@ -30,3 +30,57 @@ def test_mat2euler_roundtrip_and_reference():
     np.testing.assert_allclose(torch.stack((ax, ay, az), 1).numpy(), Z["euler"], rtol=1e-6, atol=1e-7)
     R = geo.batch_euler2mat(ax, ay, az)
     np.testing.assert_allclose(R.numpy(), Z["R_gt"], atol=1e-6)
+
+
+def test_eval_recorder_matches_per_batch_criterions():
+    """evaluate_trust_region's bookkeeping (evaluate.py:195-224) over two batches."""
+    rec = metrics.EvalRecorder()
+    B = T["R_est"].shape[0]
+    h = max(1, B // 2)
+    for sl in (slice(0, h), slice(h, B)):
+        d0 = T["depth"][sl]
+        rec.add(T["R_est"][sl], T["t_est"][sl], T["R_gt"][sl], T["t_gt"][sl], d0, T["K"][sl],
+                names=[f"f{i}" for i in range(sl.start, sl.stop)])
+    out = rec.outputs()
+    assert out["R_est"].shape == (B, 3, 3) and out["t_est"].shape == (B, 3)
+    assert out["names"] == [f"f{i}" for i in range(B)]
+    np.testing.assert_allclose(out["angular_error"], Z["ang"], rtol=1e-5, atol=1e-7)
+    np.testing.assert_allclose(out["translation_error"], Z["trs"], rtol=1e-6)
+    exp = []
+    for sl in (slice(0, h), slice(h, B)):
+        d0 = T["depth"][sl]
+        inv = (d0 == d0.min()) | (d0 == d0.max())
+        exp.append(metrics.compute_RT_EPE_loss(T["R_est"][sl], T["t_est"][sl], T["R_gt"][sl], T["t_gt"][sl], d0,
+                                               T["K"][sl], invalid=inv).numpy())
+    np.testing.assert_allclose(out["epes"], np.concatenate(exp), rtol=1e-6)
+
+
+def _fake(epes, ang, trs):
+    return {"epes": np.asarray(epes, float), "angular_error": np.asarray(ang, float),
+            "translation_error": np.asarray(trs, float)}
+
+
+def test_summarize_units_and_means(tmp_path):
+    """test_TrustRegion's table (evaluate.py:318-372): cm / degree conversion, per-keyframe
+    mean over trajectories and frame-weighted mean; pkl + CSV written where evaluate.py puts them."""
+    import pickle
+    import pandas as pd
+    res = {"fr1_desk_keyframe_1": _fake([0.01, 0.03], [0.01, 0.01], [0.02, 0.04]),
+           "fr2_xyz_keyframe_1": _fake([0.02], [0.02], [0.01]),
+           "fr1_desk_keyframe_2": _fake([0.05, 0.05, 0.05], [0.0, 0.0, 0.03], [0.1, 0.1, 0.1])}
+    table = metrics.summarize(res, [1, 2])
+    assert abs(table.loc["fr1_desk_keyframe_1", "3D EPE"] - 2.0) < 1e-9          # mean 0.02 m -> cm
+    assert abs(table.loc["fr1_desk_keyframe_2", "axis error"] - np.degrees(0.01)) < 1e-9
+    traj = table.loc["mean values of trajectories keyframe 1"]
+    assert abs(traj["3D EPE"] - (2.0 + 2.0) / 2) < 1e-9
+    frames = table.loc["mean values of frames keyframe 1"]
+    assert abs(frames["trans error"] - (3.0 * 2 + 1.0 * 1) / 3) < 1e-9
+    assert int(table.loc["fr1_desk_keyframe_2", "total frames"]) == 3
+    out = metrics.write_results(res, [1, 2], "test", root=str(tmp_path))
+    base = tmp_path / "test_results" / "nolearning"
+    with open(base / "fr1_desk_keyframe_1.pkl", "rb") as f:   # written by this test
+        back = pickle.load(f)
+    np.testing.assert_array_equal(back["epes"], res["fr1_desk_keyframe_1"]["epes"])
+    csv = pd.read_csv(base / "fr1_desk_keyframe_2.csv", index_col=0)
+    assert list(csv.index) == list(out.index)
+    np.testing.assert_allclose(csv["3D EPE"].to_numpy(float), out["3D EPE"].to_numpy(float))
