@@ -18,6 +18,8 @@ COMBINE_ICP = 0x2
 NO_UNCERTAINTY = 0x4
 FEATURES_C4 = 0x8
 SCHEDULES = {"auto": 0x00, "march": 0x10, "split": 0x20}  # DPFT_SCHED_*
+EXT_SLOT_SHIFT = 12       # DPFT_EXT_SLOT(k) = (k + 1) << 12
+EXTREMA_READY = 0x10000
 STATUS_NONFINITE = 0x1
 ABI_VERSION = 1
 
@@ -42,7 +44,8 @@ class LevelTensors(ctypes.Structure):
 EXPORTS = ("dpft_workspace_size", "dpft_ic_solve_level", "dpft_ic_iterate", "dpft_ic_residual_level",
            "dpft_residual_poses_workspace_size", "dpft_ic_residual_poses",
            "dpft_ic_reduce_only", "dpft_ic_debug_pixels", "dpft_preprocess_workspace_size",
-           "dpft_preprocess_depth", "dpft_pack_features", "dpft_version", "dpft_last_error")
+           "dpft_preprocess_depth", "dpft_pack_features", "dpft_sigma_extrema_levels", "dpft_version",
+           "dpft_last_error")
 
 _lib = None
 
@@ -78,6 +81,8 @@ def lib():
     L.dpft_preprocess_depth.argtypes = [vp, ctypes.c_int32, ctypes.c_int32, ctypes.c_int32, ctypes.c_int32,
                                         P(vp), P(vp), vp, sz, vp]
     L.dpft_preprocess_depth.restype = ctypes.c_int
+    L.dpft_sigma_extrema_levels.argtypes = [P(LevelDesc), P(LevelTensors), ctypes.c_int32, vp, sz, vp]
+    L.dpft_sigma_extrema_levels.restype = ctypes.c_int
     L.dpft_pack_features.argtypes = [vp, vp, ctypes.c_int32, ctypes.c_int32, ctypes.c_int32, ctypes.c_int32, vp]
     L.dpft_pack_features.restype = ctypes.c_int
     L.dpft_version.argtypes = []

@@ -175,6 +175,9 @@ constexpr int L_SUM = 0, L_NINV = 1, L_MN_ALL = 2, L_MN0 = 3, L_LMN = 4, L_NMN =
 // the two "blocks done" counters of the last-block finalizers, and the per-block
 // partial extrema of the sigma0 pass.  The counters are zero between calls: the
 // caller zero-fills the workspace once, every last block resets its counter.
+// kCtlMMDoneL / kCtlExtSlots: dpft_sigma_extrema_levels' per-level completion counters and
+// the per-level sigma0 extrema it leaves (DPFT_EXT_SLOT / DPFT_EXTREMA_READY)
+constexpr int kCtlMMDoneL = 10, kCtlExtSlots = 16, kMaxExtSlots = 8;
 constexpr int kCtlMin = 0, kCtlMax = 1, kCtlDone = 2, kCtlMMDone = 3, kCtlResDone = 4, kCtlD1Min = 8,
               kCtlPart = 64, kCtlPair = 1152;
 constexpr int kMaxMMBlocks = 512;
@@ -2462,8 +2465,8 @@ __global__ __launch_bounds__(kThreads) void pack_c4_kernel(const float* __restri
 
 // sigma0 batch-global min / max (algorithms.py:1976-1977).  Per-workgroup
 // partials, the last workgroup reduces them in a fixed order (no atomics on data).
-__global__ __launch_bounds__(kThreads) void minmax_kernel(const float* __restrict__ s, size_t n, uint32_t* ctrl,
-                                                          int slot) {
+__device__ void minmax_body(const float* __restrict__ s, size_t n, uint32_t* ctrl, int slot, float* part,
+                            uint32_t* done) {
   __shared__ float sm[2][4];
   float mn = INFINITY, mx = -INFINITY;
   // 16-byte loads, four in flight per thread per round (a scalar grid-stride loop
@@ -2507,12 +2510,11 @@ __global__ __launch_bounds__(kThreads) void minmax_kernel(const float* __restric
     sm[1][wave] = mx;
   }
   __syncthreads();
-  float* part = reinterpret_cast<float*>(ctrl + kCtlPart);
   if (threadIdx.x == 0) {
     st_ag(part + 2 * blockIdx.x, fminf(fminf(sm[0][0], sm[0][1]), fminf(sm[0][2], sm[0][3])));
     st_ag(part + 2 * blockIdx.x + 1, fmaxf(fmaxf(sm[1][0], sm[1][1]), fmaxf(sm[1][2], sm[1][3])));
   }
-  if (!block_is_last(ctrl + kCtlMMDone, 1u, gridDim.x)) return;
+  if (!block_is_last(done, 1u, gridDim.x)) return;
   if (threadIdx.x < 64) {
     mn = INFINITY;
     mx = -INFINITY;
@@ -2529,6 +2531,24 @@ __global__ __launch_bounds__(kThreads) void minmax_kernel(const float* __restric
       ctrl[slot + 1] = enc_ord(mx);
     }
   }
+}
+
+__global__ __launch_bounds__(kThreads) void minmax_kernel(const float* __restrict__ s, size_t n, uint32_t* ctrl,
+                                                          int slot) {
+  minmax_body(s, n, ctrl, slot, reinterpret_cast<float*>(ctrl + kCtlPart), ctrl + kCtlMMDone);
+}
+
+// Every level's sigma0 extrema in one launch (blockIdx.y = level): one pose-independent
+// pre-pass per pyramid solve instead of one launch per level.
+struct MMLevels {
+  const float* s[4];
+  size_t n[4];
+  int slot[4];
+};
+__global__ __launch_bounds__(kThreads) void minmax_levels_kernel(MMLevels a, uint32_t* ctrl) {
+  const int l = blockIdx.y;
+  minmax_body(a.s[l], a.n[l], ctrl, a.slot[l], reinterpret_cast<float*>(ctrl + kCtlPart) + 2 * l * gridDim.x,
+              ctrl + kCtlMMDoneL + l);
 }
 
 // ============================================================ depth preprocessing
@@ -2648,6 +2668,10 @@ int check_desc(const DpftLevelDesc* d) {
   if (d->B > kMaxPairs) return fail(DPFT_E_INVALID, "B=%d exceeds %d pairs per call", d->B, kMaxPairs);
   if ((d->flags & DPFT_COMBINE_ICP) && !(d->icp_weight == d->icp_weight))
     return fail(DPFT_E_INVALID, "icp_weight is NaN");
+  if (((d->flags & DPFT_EXT_SLOT_MASK) >> DPFT_EXT_SLOT_SHIFT) > (uint32_t)kMaxExtSlots)
+    return fail(DPFT_E_INVALID, "extrema slot out of range");
+  if ((d->flags & DPFT_EXTREMA_READY) && !(d->flags & DPFT_EXT_SLOT_MASK))
+    return fail(DPFT_E_INVALID, "EXTREMA_READY needs an extrema slot (DPFT_EXT_SLOT)");
   if ((d->flags & DPFT_NO_UNCERTAINTY) && (d->flags & (DPFT_REMOVE_TRU_SIGMA | DPFT_COMBINE_ICP)))
     return fail(DPFT_E_INVALID, "NO_UNCERTAINTY (IC tracker) excludes REMOVE_TRU_SIGMA and COMBINE_ICP");
   if ((d->flags & DPFT_FEATURES_C4) && (d->C % 4 != 0 || (d->Cs != 1 && !(d->flags & DPFT_NO_UNCERTAINTY))))
@@ -2723,7 +2747,8 @@ IterParams make_params(const DpftLevelDesc& d, const DpftLevelTensors& tt, const
   p.nblocks = g.nblocks;
   p.flags = d.flags;
   p.ctrl = reinterpret_cast<uint32_t*>(ws);
-  p.ext = p.ctrl + kCtlMin;
+  const int xslot = (int)((d.flags & DPFT_EXT_SLOT_MASK) >> DPFT_EXT_SLOT_SHIFT);  // 0: none
+  p.ext = p.ctrl + (xslot ? kCtlExtSlots + 2 * (xslot - 1) : kCtlMin);
   p.rec = reinterpret_cast<float*>(static_cast<char*>(ws) + rec_offset(d));
   // rows per step of the reduce kernel (4 waves x rows per lane of the instantiation launched)
   p.rps = 4 * ((d.flags & DPFT_FEATURES_C4) ? kRPL4 : (d.Cs == 1 || (d.flags & DPFT_NO_UNCERTAINTY)) ? kRPL : 1);
@@ -2765,8 +2790,11 @@ int minmax_into(const float* src, size_t n, uint32_t* ctrl, int slot, hipStream_
 int launch_minmax(const DpftLevelDesc& d, const DpftLevelTensors& tt, void* ws, hipStream_t st) {
   uint32_t* ctrl = reinterpret_cast<uint32_t*>(ws);
   int rc;
-  if (d.flags & DPFT_REMOVE_TRU_SIGMA) {
-    if ((rc = minmax_into(tt.s0, (size_t)d.B * d.Cs * d.H * d.W, ctrl, kCtlMin, st))) return rc;
+  if ((d.flags & DPFT_REMOVE_TRU_SIGMA) && !(d.flags & DPFT_EXTREMA_READY)) {
+    const int xslot = (int)((d.flags & DPFT_EXT_SLOT_MASK) >> DPFT_EXT_SLOT_SHIFT);
+    if ((rc = minmax_into(tt.s0, (size_t)d.B * d.Cs * d.H * d.W, ctrl, xslot ? kCtlExtSlots + 2 * (xslot - 1) : kCtlMin,
+                          st)))
+      return rc;
   }
   if (d.flags & DPFT_COMBINE_ICP) {
     const size_t n = (size_t)d.B * d.H * d.W;
@@ -3016,6 +3044,37 @@ int dpft_ic_debug_pixels(const DpftLevelDesc* desc, const DpftLevelTensors* tt, 
   hipLaunchKernelGGL(ic_debug_pixels_kernel, dim3((n + kThreads - 1) / kThreads), dim3(kThreads), 0,
                      static_cast<hipStream_t>(hip_stream), p, out);
   return hip_check("ic_debug_pixels_kernel");
+}
+
+int dpft_sigma_extrema_levels(const DpftLevelDesc* descs, const DpftLevelTensors* tensors, int32_t levels,
+                              void* workspace, size_t workspace_bytes, void* hip_stream) {
+  if (!descs || !tensors || !workspace) return fail(DPFT_E_INVALID, "null pointer");
+  if (levels < 1 || levels > 4) return fail(DPFT_E_INVALID, "levels=%d outside [1, 4]", levels);
+  MMLevels a;
+  size_t nmax = 0;
+  for (int l = 0; l < 4; ++l) {
+    a.s[l] = nullptr;
+    a.n[l] = 0;
+    a.slot[l] = 0;
+  }
+  for (int l = 0; l < levels; ++l) {
+    const DpftLevelDesc& d = descs[l];
+    int rc = check_desc(&d);
+    if (rc) return rc;
+    const int xslot = (int)((d.flags & DPFT_EXT_SLOT_MASK) >> DPFT_EXT_SLOT_SHIFT);
+    if (!xslot) return fail(DPFT_E_INVALID, "level %d has no extrema slot (DPFT_EXT_SLOT)", l);
+    if (!tensors[l].s0) return fail(DPFT_E_INVALID, "level %d: null sigma0", l);
+    if (workspace_bytes < ws_need(d)) return fail(DPFT_E_WORKSPACE, "workspace %zu < %zu", workspace_bytes, ws_need(d));
+    a.s[l] = tensors[l].s0;
+    a.n[l] = (size_t)d.B * d.Cs * d.H * d.W;
+    a.slot[l] = kCtlExtSlots + 2 * (xslot - 1);
+    nmax = std::max(nmax, a.n[l]);
+  }
+  const int grid = (int)std::min<size_t>((nmax + kThreads * 16 - 1) / (kThreads * 16), kMMGrid);
+  static_assert(4 * 2 * kMMGrid <= 2 * kMaxMMBlocks, "per-level minmax partials");
+  hipLaunchKernelGGL(minmax_levels_kernel, dim3(grid, levels), dim3(kThreads), 0, static_cast<hipStream_t>(hip_stream), a,
+                     static_cast<uint32_t*>(workspace));
+  return hip_check("minmax_levels_kernel");
 }
 
 size_t dpft_preprocess_workspace_size(void) { return kCtrlBytes; }

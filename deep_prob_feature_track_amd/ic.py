@@ -301,16 +301,34 @@ class PyramidSolver:
                                         obj_mask0=d.get("obj_mask0"), obj_mask1=d.get("obj_mask1"),
                                         depth0=d.get("depth0"), depth1=d.get("depth1"), combine_icp=combine_icp,
                                         icp_weight=icp_weight, status=self.status, schedule=schedule))
+        # One pose-independent pre-pass for every level's sigma0 extrema (truncated
+        # sigma): each level keeps them in its own workspace slot and skips the
+        # per-level min/max launch (dpft_sigma_extrema_levels, DPFT_EXTREMA_READY).
+        # Not with combine_icp (its depth1 pass shares the min/max scratch words).
+        self.extrema_prepass = bool(remove_tru_sigma) and not combine_icp and len(self.calls) <= 4
+        if self.extrema_prepass:
+            for l, c in enumerate(self.calls):
+                c.desc.flags |= ((l + 1) << N.EXT_SLOT_SHIFT) | N.EXTREMA_READY
+            self._descs = (N.LevelDesc * len(self.calls))(*[c.desc for c in self.calls])
+            self._tens = (N.LevelTensors * len(self.calls))(*[c.tens for c in self.calls])
         nbytes = max(c.ws_bytes for c in self.calls)
         self.ws = torch.zeros(nbytes, dtype=torch.uint8, device=dev)  # private: safe to capture; zeroed (counters)
         self.ws_bytes = nbytes
         self.device = dev
         self.B = self.calls[0].B
 
+    def prepare_extrema(self):
+        """The sigma0 extrema of every level in one launch (run() does this first)."""
+        if self.extrema_prepass:
+            rc = N.lib().dpft_sigma_extrema_levels(self._descs, self._tens, len(self.calls), _ptr(self.ws),
+                                                   self.ws_bytes, _stream(self.device))
+            N.check(rc, "dpft_sigma_extrema_levels")
+
     def run(self, R, t):
         """In place: R [B,3,3], t [B,3] fp32 contiguous device buffers."""
         L = N.lib()
         st = _stream(self.device)
+        self.prepare_extrema()
         for c in reversed(self.calls):
             rc = L.dpft_ic_solve_level(ctypes.byref(c.desc), ctypes.byref(c.tens), _ptr(R), _ptr(t), None, None,
                                        _ptr(self.ws), self.ws_bytes, st)

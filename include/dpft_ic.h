@@ -73,6 +73,15 @@ extern "C" {
 #define DPFT_SCHED_MARCH   0x10u
 #define DPFT_SCHED_SPLIT   0x20u
 
+/* Per-level sigma0 extrema slots (pyramid solves, one pre-pass for all levels):
+ * DPFT_EXT_SLOT(k) (k = 0..7) keeps this level's extrema in workspace slot k;
+ * DPFT_EXTREMA_READY: dpft_sigma_extrema_levels already filled the slot, so the
+ * first iteration of the level does not recompute them.                          */
+#define DPFT_EXT_SLOT_SHIFT 12
+#define DPFT_EXT_SLOT_MASK  0xF000u
+#define DPFT_EXT_SLOT(k)    ((((uint32_t)(k)) + 1u) << DPFT_EXT_SLOT_SHIFT)
+#define DPFT_EXTREMA_READY  0x10000u
+
 /* device status word bits */
 #define DPFT_STATUS_NONFINITE 0x1u /* a JtJ / JtR reduction was not finite         */
 
@@ -160,6 +169,16 @@ size_t dpft_residual_poses_workspace_size(const DpftLevelDesc* desc, int32_t n_p
 int dpft_ic_residual_poses(const DpftLevelDesc* desc, const DpftLevelTensors* tensors, int32_t n_poses,
                            const float* R, const float* t, float* loss,
                            void* workspace, size_t workspace_bytes, void* hip_stream);
+
+/*
+ * The batch-global sigma0 min / max of every level of a pyramid (the truncated-sigma
+ * masks' pose-independent half, algorithms.py:1976-1977) in ONE launch, into the
+ * workspace slots named by each descriptor's DPFT_EXT_SLOT.  The levels then run with
+ * DPFT_EXTREMA_READY.  Replaces one min/max launch per level (LeastSquareTracking.py:
+ * 349-445 solves 4 levels per pair).  All levels must share `workspace`.
+ */
+int dpft_sigma_extrema_levels(const DpftLevelDesc* descs, const DpftLevelTensors* tensors, int32_t levels,
+                              void* workspace, size_t workspace_bytes, void* hip_stream);
 
 /* Kernel-only timing hook for the roofline: launch ONLY the fused residual +
  * Jacobian + normal-equation kernel (no finalize), using the sigma0 extrema a

@@ -230,3 +230,33 @@ def test_c4_schedules_random(schedule, C, H, W, no_unc, masks):
     torch.testing.assert_close(b[3], a[3], rtol=1e-4, atol=1e-5 * a[3].abs().max().item())
     torch.testing.assert_close(b[0], a[0], rtol=0, atol=2e-5)
     torch.testing.assert_close(b[1], a[1], rtol=0, atol=2e-5)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("packed", [False, True])
+def test_pyramid_solver_extrema_prepass_bit_identical(packed):
+    """PyramidSolver's one-launch sigma0 extrema pre-pass (per-level workspace slots,
+    DPFT_EXTREMA_READY) against the per-level path (dpft_ic_solve_level computing the
+    extrema itself): the extrema are exact min / max, so the poses are bit-identical."""
+    from deep_prob_feature_track_amd import ic
+    dev = _dev()
+    case, z = golden_io.load("cfg2_640x480_c32")
+    lv = golden_io.levels_torch(case, torch.float32, dev)
+    R0, t0 = golden_io.init_pose(case, torch.float32, dev)
+    K = torch.from_numpy(case["K"]).to(dev)
+    pk = (lambda x: ic.pack_features(x)) if packed else (lambda x: x)
+    levels = [dict(x0=pk(d["f0"]), x1=pk(d["f1"]), invD0=d["invD0"], invD1=d["invD1"], sigma0=d["s0"],
+                   sigma1=d["s1"]) for d in lv]
+    solver = ic.PyramidSolver(levels, K, iters=3, remove_tru_sigma=True)
+    assert solver.extrema_prepass
+    R, t = R0.clone().contiguous(), t0.reshape(-1, 3).clone().contiguous()
+    solver.run(R, t)
+    Rs, ts = R0.clone(), t0.reshape(-1, 3, 1).clone()
+    for l in reversed(range(len(levels))):
+        d = levels[l]
+        Rs, ts = ic.solve_level((Rs, ts), d["x0"], d["x1"], d["invD0"], d["invD1"], K / 2 ** l, d["sigma0"],
+                                d["sigma1"], iters=3, remove_tru_sigma=True)
+    torch.cuda.synchronize()
+    assert torch.equal(R, Rs) and torch.equal(t, ts.reshape(-1, 3))
+    for prec in ("f32", "f64"):
+        assert np.abs(R.cpu().numpy() - z[f"{prec}_R"][-1]).max() <= SE3_TOL

@@ -32,6 +32,7 @@ R = torch.eye(3, device=dev).repeat(a.batch, 1, 1).contiguous()
 t = torch.zeros(a.batch, 3, device=dev)
 import ctypes
 from deep_prob_feature_track_amd import _native as N
+solver.prepare_extrema()  # per-level sigma0 extrema slots (the levels run with EXTREMA_READY)
 for level in ([a.level] if a.level >= 0 else range(len(solver.calls))):
     c = solver.calls[level]
     rc = N.lib().dpft_ic_iterate(ctypes.byref(c.desc), ctypes.byref(c.tens), ic._ptr(R.clone()), ic._ptr(t.clone()),
