@@ -33,22 +33,35 @@ def main():
     rows = sorted(csv.DictReader(open(a.trace)), key=lambda r: int(r["Start_Timestamp"]))
     mm_grids = sorted({int(r["Grid_Size_X"]) for r in rows if "minmax" in r["Kernel_Name"]})
     top = 3  # coarsest level of the 4-level bench pyramid
+    ITERS = 3
+    n_red = None
     groups = collections.defaultdict(list)
     level = None
     timeline, cur, solves = [], [], []
     for r in rows:
         name = short(r["Kernel_Name"])
         dur = (int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e3
-        if "minmax" in name:
-            # the smallest sigma0 pass opens level 3; each later one opens the next finer
-            # level (levels 2..0 may share a capped grid)
+        if name.startswith("minmax_levels"):
+            # one sigma0 pre-pass for all levels opens a solve; levels then advance every
+            # ITERS reduce launches (extra level-0 launches after the solve stay level 0)
+            level, n_red = top, 0
+            if cur:
+                solves.append(cur)
+                cur = []
+        elif "minmax" in name:
+            # per-level sigma0 pass (older traces / solves without the pre-pass): the
+            # smallest opens level 3, each later one the next finer level
             if int(r["Grid_Size_X"]) == mm_grids[0]:
                 level = top
             else:
                 level = max((level if level is not None else top) - 1, 0)
+            n_red = None
             if level == top and cur:
                 solves.append(cur)
                 cur = []
+        elif n_red is not None and level is not None and name.startswith(("ic_reduce", "ic_split")):
+            level = max(top - n_red // ITERS, 0)
+            n_red += 1
         if level is None:
             continue
         layout = "nchw" if name.endswith("false>") else "c4"
