@@ -260,3 +260,28 @@ def test_pyramid_solver_extrema_prepass_bit_identical(packed):
     assert torch.equal(R, Rs) and torch.equal(t, ts.reshape(-1, 3))
     for prec in ("f32", "f64"):
         assert np.abs(R.cpu().numpy() - z[f"{prec}_R"][-1]).max() <= SE3_TOL
+
+
+@pytest.mark.gpu
+def test_pyramid_solver_iterate_uses_ready_extrema():
+    """bench.py times PyramidSolver.iterate(first=True) after run(): with
+    DPFT_EXTREMA_READY it reads the level's slot filled by the pre-pass, and must match a
+    standalone iteration that computes the extrema itself, bit for bit."""
+    from deep_prob_feature_track_amd import ic
+    dev = _dev()
+    case, z = golden_io.load("cfg2_640x480_c32")
+    lv = golden_io.levels_torch(case, torch.float32, dev)
+    R0, t0 = golden_io.init_pose(case, torch.float32, dev)
+    K = torch.from_numpy(case["K"]).to(dev)
+    levels = [dict(x0=ic.pack_features(d["f0"]), x1=ic.pack_features(d["f1"]), invD0=d["invD0"], invD1=d["invD1"],
+                   sigma0=d["s0"], sigma1=d["s1"]) for d in lv]
+    solver = ic.PyramidSolver(levels, K, iters=3, remove_tru_sigma=True)
+    R, t = R0.clone().contiguous(), t0.reshape(-1, 3).clone().contiguous()
+    solver.run(R, t)
+    Ra, ta = R.clone(), t.clone()
+    solver.iterate(0, Ra, ta, first=True)
+    d = levels[0]
+    Rb, tb, _, _, _ = ic.iterate((R.clone(), t.reshape(-1, 3, 1).clone()), d["x0"], d["x1"], d["invD0"], d["invD1"], K,
+                                 d["sigma0"], d["sigma1"], first=True, remove_tru_sigma=True)
+    torch.cuda.synchronize()
+    assert torch.equal(Ra, Rb) and torch.equal(ta, tb.reshape(-1, 3))
