@@ -32,8 +32,8 @@ HBM_PEAK_GBS = 8000.0  # MI355X spec, MI355X_MICROARCH.md chip table
 def parse():
     p = argparse.ArgumentParser()
     p.add_argument("--gpus", type=int, default=1)
-    p.add_argument("--steps", type=int, default=20)
-    p.add_argument("--warmup", type=int, default=3)
+    p.add_argument("--steps", type=int, default=100)
+    p.add_argument("--warmup", type=int, default=10)
     p.add_argument("--batch-per-gpu", type=int, default=8)
     p.add_argument("--kernel-reps", type=int, default=50)
     p.add_argument("--no-cpu-baseline", action="store_true")
