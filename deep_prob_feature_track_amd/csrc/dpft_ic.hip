@@ -131,7 +131,7 @@ constexpr int kRingM = DPFT_RING_M;       // quads in flight on the marching pat
 #define DPFT_UNROLL_Q 1  // marching path: the quad loop straight-line (static quad indices)
 #endif
 #ifndef DPFT_RING_Q
-#define DPFT_RING_Q 3
+#define DPFT_RING_Q 4
 #endif
 constexpr int kRingQ = DPFT_RING_Q;  // straight-line marching quad loop: quads in flight
 #ifndef DPFT_LATE_TERMS
