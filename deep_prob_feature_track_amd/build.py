@@ -1,5 +1,14 @@
-"""Build libdpft_ic.so in-tree for gfx950 (hipcc cross-compiles without a GPU)."""
+"""Build libdpft_ic.so in-tree for gfx950 (hipcc cross-compiles without a GPU).
+
+The compile also emits the compiler's per-kernel resource report
+(-Rpass-analysis=kernel-resource-usage); the build fails if a hot kernel lost its
+occupancy -- the channel-quad marching kernels sit a few VGPRs under the 256 that
+allow 2 waves per SIMD (one register more halves their residency and, measured,
+costs ~70 % on the level-0 launch), and nothing at run time would notice: the grid
+is sized from the occupancy query, so results stay right and only speed drops.
+"""
 import os
+import re
 import subprocess
 import sys
 
@@ -11,16 +20,58 @@ INC = os.path.join(ROOT, "include")
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 ARCH = os.environ.get("DPFT_OFFLOAD_ARCH", "gfx950")
 
+# kernel-name pattern -> minimum waves per SIMD, no register spills
+OCCUPANCY_FLOOR = {
+    r"^void \(anonymous namespace\)::ic_reduce_kernel<(16|32), true, (true|false), [012], true>": 2,
+    r"^void \(anonymous namespace\)::ic_split_kernel<": 4,
+}
+
+
+def kernel_resources(stderr):
+    """Parse -Rpass-analysis=kernel-resource-usage remarks -> {demangled name: {field: int}}."""
+    out, cur = {}, None
+    for line in stderr.splitlines():
+        m = re.search(r"remark:\s+(Function Name|VGPRs|AGPRs|VGPRs Spill|Occupancy \[waves/SIMD\]|"
+                      r"ScratchSize \[bytes/lane\]|LDS Size \[bytes/block\]): (\S+)", line)
+        if not m:
+            continue
+        key, val = m.group(1), m.group(2)
+        if key == "Function Name":
+            name = subprocess.run(["c++filt", val], capture_output=True, text=True).stdout.strip() or val
+            cur = out.setdefault(name, {})
+        elif cur is not None:
+            cur[key] = int(val)
+    return out
+
+
+def check_occupancy(res):
+    bad = []
+    for pat in OCCUPANCY_FLOOR:
+        if not any(re.search(pat, name) for name in res):
+            bad.append(f"no kernel matches {pat!r} (renamed? the guard would check nothing)")
+    for name, r in res.items():
+        for pat, floor in OCCUPANCY_FLOOR.items():
+            if re.search(pat, name):
+                occ, spill = r.get("Occupancy [waves/SIMD]", 0), r.get("VGPRs Spill", 0)
+                if occ < floor or spill:
+                    bad.append(f"{name}: {r.get('VGPRs')} VGPRs, {occ} waves/SIMD (floor {floor}), {spill} spilled")
+    if bad:
+        raise RuntimeError("occupancy regression:\n  " + "\n  ".join(bad))
+
 
 def build(force=False, verbose=False):
     deps = [SRC, os.path.join(INC, "dpft_ic.h"), __file__]
     if not force and os.path.exists(OUT) and os.path.getmtime(OUT) >= max(os.path.getmtime(d) for d in deps):
         return OUT
     cmd = [HIPCC, f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-shared", "-fPIC", f"-I{INC}",
-           "-o", OUT + ".tmp", SRC]
+           "-Rpass-analysis=kernel-resource-usage", "-o", OUT + ".tmp", SRC]
     if verbose:
         print(" ".join(cmd), file=sys.stderr)
-    subprocess.run(cmd, check=True)
+    r = subprocess.run(cmd, capture_output=True, text=True)
+    if r.returncode != 0:
+        sys.stderr.write(r.stderr)
+        raise subprocess.CalledProcessError(r.returncode, cmd)
+    check_occupancy(kernel_resources(r.stderr))
     os.replace(OUT + ".tmp", OUT)
     return OUT
 

@@ -89,7 +89,7 @@ constexpr int kRowsPerStep = 4;        // one row per wave per step
 #define DPFT_MAX_STEPS 4
 #endif
 #ifndef DPFT_MIN_WAVES
-#define DPFT_MIN_WAVES 1
+#define DPFT_MIN_WAVES 1  // (2 pins <= 256 VGPRs but schedules the marching loop 4-5 % slower; build.py checks instead)
 #endif
 #ifndef DPFT_MARCH
 #define DPFT_MARCH 1
@@ -101,7 +101,7 @@ constexpr bool kMarch = DPFT_MARCH != 0;  // channel-quad reduce: row-marching w
 #ifndef DPFT_SPLIT_MAX_PIXELS
 #define DPFT_SPLIT_MAX_PIXELS 40000
 #endif
-constexpr long kSplitMaxPixels = DPFT_SPLIT_MAX_PIXELS;
+constexpr long kSplitMaxPixels = DPFT_SPLIT_MAX_PIXELS;  // channel-quad levels up to this size per pair: ic_split_kernel
 #ifndef DPFT_SPLIT_SEPFIN
 #define DPFT_SPLIT_SEPFIN 1
 #endif
@@ -109,14 +109,14 @@ constexpr bool kSplitSepFin = DPFT_SPLIT_SEPFIN != 0;
 #ifndef DPFT_SEPFIN_MAX_PIXELS
 #define DPFT_SEPFIN_MAX_PIXELS 0
 #endif
-constexpr long kSepFinMaxPixels = DPFT_SEPFIN_MAX_PIXELS;  // ic_reduce_kernel levels finalized by a separate launch  // levels up to this size per pair: ic_split_kernel  // channel-quad U_IC / IC: workgroup-marching kernel
+constexpr long kSepFinMaxPixels = DPFT_SEPFIN_MAX_PIXELS;  // ic_reduce_kernel levels finalized by a separate launch
 #ifndef DPFT_MARCH_ROWS
 #define DPFT_MARCH_ROWS 1
 #endif
 #ifndef DPFT_MARCH_CSPLIT
 #define DPFT_MARCH_CSPLIT 1
 #endif
-constexpr int kMarchCSplit = DPFT_MARCH_CSPLIT;
+constexpr int kMarchCSplit = DPFT_MARCH_CSPLIT;  // waves sharing a marching band (channel quads split)
 #ifndef DPFT_MARCH_REVERSE
 #define DPFT_MARCH_REVERSE 1
 #endif
@@ -124,7 +124,7 @@ constexpr bool kMarchReverse = DPFT_MARCH_REVERSE != 0;  // honour DPFT_ITER_REV
 #ifndef DPFT_MARCH_SKEW
 #define DPFT_MARCH_SKEW 10
 #endif
-constexpr int kMarchSkew = DPFT_MARCH_SKEW;  // band-size skew of the marching schedule (64ths)  // waves sharing a marching band (channel quads split)
+constexpr int kMarchSkew = DPFT_MARCH_SKEW;  // band-size skew of the marching schedule (64ths, 0..63)
 constexpr int kMarchRows = DPFT_MARCH_ROWS;  // rows per marching step (1, or 2: -10 % f1 traffic, +11 % VALU, 4 % slower)
 constexpr int kRingM = DPFT_RING_M;       // quads in flight on the marching path (kRingM - 1 ahead)
 #ifndef DPFT_UNROLL_Q
@@ -181,6 +181,12 @@ constexpr int kCtlMMDoneL = 10, kCtlExtSlots = 16, kMaxExtSlots = 8;
 constexpr int kCtlMin = 0, kCtlMax = 1, kCtlDone = 2, kCtlMMDone = 3, kCtlResDone = 4, kCtlD1Min = 8,
               kCtlPart = 64, kCtlPair = 1152;
 constexpr int kMaxMMBlocks = 512;
+// pair_reduce2's LDS scratch: 42 fields x 65 quad rows (the extrema exchange overlaps it)
+constexpr int kFinScratch = 42 * 65;
+// cache-policy operand of the raw buffer intrinsics: sc1 (agent-coherent; gfx940+ bit 4)
+constexpr int kAuxSc1 = 16;
+// DPFT_TAIL_PROF builds only: per-workgroup finish stamps, per-pair reduce stamps, batch stamps
+constexpr int kCtlTail = 3264, kTailWG = 768, kTailPairs = 16;
 #ifndef DPFT_MM_GRID
 #define DPFT_MM_GRID 128
 #endif
@@ -191,11 +197,13 @@ constexpr int kMaxMMBlocks = 512;
 // Its last-workgroup reduction serialises one counter arrival per workgroup.
 constexpr int kMMGrid = DPFT_MM_GRID, kMMLoads = DPFT_MM_LOADS;
 static_assert(kMMGrid <= kMaxMMBlocks, "minmax partials");
+static_assert(DPFT_MARCH_SKEW >= 0 && DPFT_MARCH_SKEW < 64, "band skew in 64ths");
 constexpr int kMaxPairs = 2048;  // per call (one completion counter per pair)
 constexpr int kMaxGrid = 4096;   // reduce-kernel workgroups (resident capacity is far below)
 constexpr size_t kCtrlBytes = 16384;
 static_assert((kCtlPart + 2 * kMaxMMBlocks) * 4 <= kCtlPair * 4, "ctrl area");
 static_assert((kCtlPair + kMaxPairs) * 4 <= kCtrlBytes, "ctrl area");
+static_assert(kCtlTail >= kCtlPair + kMaxPairs && (kCtlTail + kTailWG + 2 * kTailPairs + 2) * 4 <= kCtrlBytes, "tail stamps");
 // per-pair record (fp64) written by the last workgroup of each pair
 constexpr int P_S = 0;        // 28: JtJ upper (21), JtR (6), #invalid
 constexpr int P_CMN = 28;     // 7: JtR / count corrections of the blocks at the pair's min sigma_r ch0
@@ -859,160 +867,6 @@ __device__ void block_minmax2(float& mn_a, float& mx_a, float& mn_b, float& mx_b
   mx_b = fmaxf(fmaxf(sm[3][0], sm[3][1]), fmaxf(sm[3][2], sm[3][3]));
 }
 
-// Run by the last workgroup of pair b: reduce its per-workgroup records into one
-// fp64 pair record in ONE load round trip.  Threads 0-127 take the 21 JtJ
-// components of record tid (+128, ...), threads 128-255 the 6 JtR components, the
-// invalid count and the truncated-sigma extremum fields; per-thread fp64 sums and
-// online extremum merges (fixed record order), then fixed xor-tree wave
-// reductions and a fixed two-wave combine: deterministic for any finishing order.
-// The corrections of the records attaining the pair's extremum of sigma_r ch0 are
-// kept apart: whether they apply depends on the batch-global extremum.
-struct ExtD {
-  float v;     // extremum of sigma_r channel 0
-  double c[7]; // JtR corrections (6) + count of the pixels attaining it
-};
-template <bool MIN>
-__device__ __forceinline__ void extd_merge(ExtD& a, float v, const double* c) {
-  if (MIN ? (v < a.v) : (v > a.v)) {
-    a.v = v;
-#pragma unroll
-    for (int i = 0; i < 7; ++i) a.c[i] = c[i];
-  } else if (v == a.v) {
-#pragma unroll
-    for (int i = 0; i < 7; ++i) a.c[i] += c[i];
-  }
-}
-template <bool MIN>
-__device__ __forceinline__ void extd_wave_reduce(ExtD& e) {
-  for (int off = 32; off > 0; off >>= 1) {
-    const float v = __shfl_xor(e.v, off);
-    double c[7];
-#pragma unroll
-    for (int i = 0; i < 7; ++i) c[i] = __shfl_xor(e.c[i], off);
-    // both partners apply the same (commutative) rule to the same pair of values
-    extd_merge<MIN>(e, v, c);
-  }
-}
-
-__device__ void pair_reduce(const FinParams& q, int b) {
-  __shared__ double shs[2][21];
-  __shared__ double shr[2][7];
-  __shared__ float shv[2][4];
-  __shared__ double shc[2][2][7];
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const bool tru = (q.flags & DPFT_REMOVE_TRU_SIGMA) != 0;
-  const float* rec = q.rec + (size_t)b * q.nbpp * kRec;  // slots of pair b's workgroups
-  const int n = q.nbpp;
-  double* pr = q.prec + (size_t)b * kPRec;
-  // (workgroups wider than kThreads: threads >= kThreads only take part in the barriers)
-  if (tid < 128) {
-    double s[21];
-#pragma unroll
-    for (int i = 0; i < 21; ++i) s[i] = 0.0;
-    for (int k = tid; k < n; k += 128) {
-      float v[21];
-      const float* r = rec + (size_t)k * kRec;
-#pragma unroll
-      for (int i = 0; i < 21; ++i) v[i] = ld_ag(r + i);
-#pragma unroll
-      for (int i = 0; i < 21; ++i) s[i] += (double)v[i];
-    }
-#pragma unroll
-    for (int i = 0; i < 21; ++i) s[i] = wave_sum_d(s[i]);
-    if (lane == 0)
-#pragma unroll
-      for (int i = 0; i < 21; ++i) shs[wave][i] = s[i];
-  } else if (tid < kThreads) {
-    double s[7];
-#pragma unroll
-    for (int i = 0; i < 7; ++i) s[i] = 0.0;
-    ExtD emn, emx;
-    emn.v = INFINITY;
-    emx.v = -INFINITY;
-#pragma unroll
-    for (int i = 0; i < 7; ++i) emn.c[i] = emx.c[i] = 0.0;
-    float mn_all = INFINITY, mx_all = -INFINITY;
-    for (int k = tid - 128; k < n; k += 128) {
-      const float* r = rec + (size_t)k * kRec;
-      float v[7], cn[7], cx[7], m0 = 0.f, x0 = 0.f, ma = 0.f, xa = 0.f;
-#pragma unroll
-      for (int i = 0; i < 7; ++i) v[i] = ld_ag(r + 21 + i);
-      if (tru) {
-#pragma unroll
-        for (int i = 0; i < 7; ++i) {
-          cn[i] = ld_ag(r + R_CMN + i);  // R_CMN + 6 == R_NMN
-          cx[i] = ld_ag(r + R_CMX + i);  // R_CMX + 6 == R_NMX
-        }
-        m0 = ld_ag(r + R_MN0);
-        x0 = ld_ag(r + R_MX0);
-        ma = ld_ag(r + R_MN_ALL);
-        xa = ld_ag(r + R_MX_ALL);
-      }
-#pragma unroll
-      for (int i = 0; i < 7; ++i) s[i] += (double)v[i];
-      if (tru) {
-        double dn[7], dx[7];
-#pragma unroll
-        for (int i = 0; i < 7; ++i) {
-          dn[i] = (double)cn[i];
-          dx[i] = (double)cx[i];
-        }
-        extd_merge<true>(emn, m0, dn);
-        extd_merge<false>(emx, x0, dx);
-        mn_all = fminf(mn_all, ma);
-        mx_all = fmaxf(mx_all, xa);
-      }
-    }
-#pragma unroll
-    for (int i = 0; i < 7; ++i) s[i] = wave_sum_d(s[i]);
-    if (tru) {
-      extd_wave_reduce<true>(emn);
-      extd_wave_reduce<false>(emx);
-      for (int off = 32; off > 0; off >>= 1) {
-        mn_all = fminf(mn_all, __shfl_xor(mn_all, off));
-        mx_all = fmaxf(mx_all, __shfl_xor(mx_all, off));
-      }
-    }
-    const int w = wave - 2;
-    if (lane == 0) {
-#pragma unroll
-      for (int i = 0; i < 7; ++i) {
-        shr[w][i] = s[i];
-        shc[w][0][i] = emn.c[i];
-        shc[w][1][i] = emx.c[i];
-      }
-      shv[w][0] = emn.v;
-      shv[w][1] = emx.v;
-      shv[w][2] = mn_all;
-      shv[w][3] = mx_all;
-    }
-  }
-  __syncthreads();
-  if (tid < 21) {
-    st_ag(pr + P_S + tid, shs[0][tid] + shs[1][tid]);
-  } else if (tid < 28) {
-    st_ag(pr + P_S + tid, shr[0][tid - 21] + shr[1][tid - 21]);
-  } else if (tid == 64) {
-    ExtD e;
-    e.v = shv[0][0];
-#pragma unroll
-    for (int i = 0; i < 7; ++i) e.c[i] = shc[0][0][i];
-    extd_merge<true>(e, shv[1][0], shc[1][0]);
-    for (int i = 0; i < 7; ++i) st_ag(pr + P_CMN + i, e.c[i]);
-    st_ag(pr + P_MN0, (double)e.v);
-    st_ag(pr + P_MN_ALL, (double)fminf(shv[0][2], shv[1][2]));
-  } else if (tid == 128) {
-    ExtD e;
-    e.v = shv[0][1];
-#pragma unroll
-    for (int i = 0; i < 7; ++i) e.c[i] = shc[0][1][i];
-    extd_merge<false>(e, shv[1][1], shc[1][1]);
-    for (int i = 0; i < 7; ++i) st_ag(pr + P_CMX + i, e.c[i]);
-    st_ag(pr + P_MX0, (double)e.v);
-    st_ag(pr + P_MX_ALL, (double)fmaxf(shv[0][3], shv[1][3]));
-  }
-}
-
 // Run by the workgroup that completes the last pair: batch-global truncated-sigma
 // extrema over the pair records, corrections, then one thread per pair solves and
 // updates its pose (algorithms.py:2017-2103).
@@ -1067,6 +921,149 @@ __device__ void finalize_batch(const FinParams& q) {
   finalize_batch_from(q, [&](int b, int i) { return ld_ag(q.prec + (size_t)b * kPRec + i); });
 }
 
+// Wave min / max trees (fixed order), every value moved before each step's wait.
+// v[0], v[1]: min; v[2], v[3]: max
+__device__ __forceinline__ void wave_minmax4(float (&v)[4]) {
+  const int lane = threadIdx.x & 63;
+#pragma unroll
+  for (int off = 1; off < 64; off <<= 1) {
+    const int addr = (lane ^ off) << 2;
+    float o[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) o[i] = __int_as_float(__builtin_amdgcn_ds_bpermute(addr, __float_as_int(v[i])));
+    v[0] = fminf(v[0], o[0]);
+    v[1] = fminf(v[1], o[1]);
+    v[2] = fmaxf(v[2], o[2]);
+    v[3] = fmaxf(v[3], o[3]);
+  }
+}
+
+// Run by the last workgroup of pair b: its nbpp workgroup records -> one fp64 pair
+// record (kPRec layout) in one load round trip.  Thread t holds record t (16-byte sc1
+// loads: agent-coherent, as the records were stored); records t + 256, ... (pairs
+// with more than 256 workgroups) are folded into it in record order (sums in fp32,
+// extrema by ext_merge's ties-add rule).  The pair's sigma_r extrema decide which
+// records' truncated-sigma corrections count; then quad sums by DPP and an LDS
+// transpose reduce the 42 fields (28 without truncated sigma) column by column in
+// fp64.  Fixed order throughout: deterministic for any finishing order.  `sc`: LDS the
+// launch no longer needs, >= kFinScratch floats.
+__device__ void pair_reduce2(const FinParams& q, int b, float* sc) {
+  const bool tru = (q.flags & DPFT_REMOVE_TRU_SIGMA) != 0;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int n = q.nbpp;
+  const Rsrc rr = rsrc(q.rec + (size_t)b * n * kRec, (uint32_t)((size_t)n * kRec * sizeof(float)));
+  float f[48];
+#pragma unroll
+  for (int i = 0; i < 48; ++i) f[i] = 0.f;
+  f[R_MN_ALL] = f[R_MN0] = INFINITY;
+  f[R_MX_ALL] = f[R_MX0] = -INFINITY;
+  for (int k = tid; k < n; k += kThreads) {
+    f32x4 v[12];
+#pragma unroll
+    for (int j = 0; j < 12; ++j) v[j] = llvm_buf_load_f32x4(rr, k * kRec * 4 + 16 * j, 0, kAuxSc1);
+    const float* g = reinterpret_cast<const float*>(v);
+    if (k == tid) {
+#pragma unroll
+      for (int i = 0; i < 48; ++i) f[i] = g[i];
+      if (!tru) {
+        f[R_MN_ALL] = f[R_MN0] = INFINITY;
+        f[R_MX_ALL] = f[R_MX0] = -INFINITY;
+      }
+    } else {
+#pragma unroll
+      for (int i = 0; i < 28; ++i) f[i] += g[i];
+      if (tru) {
+        Extremum e;
+        e.all = f[R_MN_ALL];
+        e.v0 = f[R_MN0];
+        e.n = f[R_NMN];
+#pragma unroll
+        for (int i = 0; i < 6; ++i) e.c[i] = f[R_CMN + i];
+        ext_merge<true>(e, g[R_MN_ALL], g[R_MN0], g + R_CMN, g[R_NMN]);
+        f[R_MN_ALL] = e.all;
+        f[R_MN0] = e.v0;
+        f[R_NMN] = e.n;
+#pragma unroll
+        for (int i = 0; i < 6; ++i) f[R_CMN + i] = e.c[i];
+        e.all = f[R_MX_ALL];
+        e.v0 = f[R_MX0];
+        e.n = f[R_NMX];
+#pragma unroll
+        for (int i = 0; i < 6; ++i) e.c[i] = f[R_CMX + i];
+        ext_merge<false>(e, g[R_MX_ALL], g[R_MX0], g + R_CMX, g[R_NMX]);
+        f[R_MX_ALL] = e.all;
+        f[R_MX0] = e.v0;
+        f[R_NMX] = e.n;
+#pragma unroll
+        for (int i = 0; i < 6; ++i) f[R_CMX + i] = e.c[i];
+      }
+    }
+  }
+#if DPFT_TAIL_PROF
+  auto stamp = [&](int i) {
+    __builtin_amdgcn_s_waitcnt(0);
+    if (b == 0 && tid == 0) st_ag(q.pair_cnt + kCtlTail - kCtlPair + kTailWG + 2 * kTailPairs + 2 + i,
+                                  (uint32_t)wall_clock64());
+  };
+  stamp(0);
+#endif
+  // pair extrema of sigma_r first (which records' corrections count)
+  float ex[4] = {f[R_MN_ALL], f[R_MN0], f[R_MX_ALL], f[R_MX0]};
+  if (tru) {
+    wave_minmax4(ex);
+    float* scf = sc;
+    if (lane == 0)
+#pragma unroll
+      for (int i = 0; i < 4; ++i) scf[4 * wave + i] = ex[i];
+    __syncthreads();
+    ex[0] = fminf(fminf(scf[0], scf[4]), fminf(scf[8], scf[12]));
+    ex[1] = fminf(fminf(scf[1], scf[5]), fminf(scf[9], scf[13]));
+    ex[2] = fmaxf(fmaxf(scf[2], scf[6]), fmaxf(scf[10], scf[14]));
+    ex[3] = fmaxf(fmaxf(scf[3], scf[7]), fmaxf(scf[11], scf[15]));
+    __syncthreads();  // scf is reused below
+  }
+#if DPFT_TAIL_PROF
+  stamp(1);
+#endif
+  // fields in the pair-record order: 28 sums, then the 7 + 7 corrections (masked)
+  const bool use_mn = f[R_MN0] == ex[1], use_mx = f[R_MX0] == ex[3];
+  auto field = [&](int i) -> float {
+    if (i < 28) return f[i];
+    if (i < 35) return use_mn ? f[R_CMN + (i - 28)] : 0.f;  // R_CMN + 6 == R_NMN
+    return use_mx ? f[R_CMX + (i - 35)] : 0.f;              // R_CMX + 6 == R_NMX
+  };
+  const int nf = tru ? 42 : 28;
+  // quad sums by DPP (xor 1, then xor 2: ((r0 + r1) + (r2 + r3)) in every lane of the
+  // quad), then the 64 quad rows transposed through LDS ([field][65]: conflict-free
+  // columns) and summed per field in fp64, row order -- no cross-lane shuffle chains
+  float* L = sc;
+#pragma unroll
+  for (int i = 0; i < 42; ++i) {
+    float v = field(i);
+    v += __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), 0xB1, 0xf, 0xf, true));  // quad_perm 1,0,3,2
+    v += __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), 0x4E, 0xf, 0xf, true));  // quad_perm 2,3,0,1
+    if (i < nf && (tid & 3) == 0) L[i * 65 + (tid >> 2)] = v;
+  }
+#if DPFT_TAIL_PROF
+  stamp(2);
+#endif
+  __syncthreads();
+  double* pr = q.prec + (size_t)b * kPRec;
+  if (tid < nf) {
+    double v = 0.0;
+    const float* col = L + tid * 65;
+#pragma unroll 16
+    for (int r = 0; r < 64; ++r) v += (double)col[r];
+    st_ag(pr + (tid < 28 ? P_S + tid : tid < 35 ? P_CMN + (tid - 28) : P_CMX + (tid - 35)), v);
+  } else if (tid >= 64 && tid < 64 + 2 * 7 && !tru) {
+    st_ag(pr + P_CMN + (tid - 64), 0.0);  // (P_CMX follows P_CMN)
+  } else if (tid >= 128 && tid < 132) {
+    const int i = tid - 128;
+    st_ag(pr + (i == 0 ? P_MN_ALL : i == 1 ? P_MN0 : i == 2 ? P_MX_ALL : P_MX0), (double)ex[i]);
+  }
+}
+
+
 // Last workgroup of a residual launch: loss[b] = sum / (HW - #invalid)
 // (algorithms.py:2119-2137).
 __device__ void finalize_loss(const FinParams& q) {
@@ -1109,13 +1106,8 @@ __device__ void finalize_loss(const FinParams& q) {
 template <int CT, bool CS1, bool TRU, int MODE, bool C4>
 __global__ __launch_bounds__(kThreads, DPFT_MIN_WAVES) void ic_reduce_kernel(IterParams p) {
   constexpr bool ICP = MODE == 1, NOSIG = MODE == 2;
-#if DPFT_TAIL_PROF  // profiling build: launch timeline in ctrl words 16..28 (tools/kbench.py --tail)
-  if (threadIdx.x == 0) {
-    const uint32_t ts = (uint32_t)wall_clock64();
-    atomicMin(p.ctrl + 16, ts);
-    if (blockIdx.x < 512) st_ag(p.ctrl + 64 + 512 + xcd_remap(blockIdx.x, gridDim.x), ts);
-  }
-#endif
+  // (DPFT_TAIL_PROF, profiling build: finish timeline in ctrl words 16..28 and 64.., stamped only
+  // after the pass -- a stamp at the start costs the main loop registers; tools/kbench.py --tail)
   static_assert(!C4 || CS1, "the channel-quad layout needs one sigma plane");
   constexpr int R = C4 ? ((kMarch && CT > 0) ? 1 : kRPL4) : (CS1 ? kRPL : 1);  // rows per lane
   constexpr float kFill = NOSIG ? 1e-3f : 1e-6f;  // weighted residual of invalid pixels
@@ -1124,6 +1116,10 @@ __global__ __launch_bounds__(kThreads, DPFT_MIN_WAVES) void ic_reduce_kernel(Ite
   __shared__ float red[4][kRec];
   constexpr bool kWin = C4 && kMarch && CT > 0;
   __shared__ f32x4 lds_win[kWin ? 4 : 1][kWin ? 2 * (CT / 4) * 64 : 1];  // used: 2 x NQW quads per wave
+  // pair_reduce2 scratch where neither the window nor the extremum buffer is there to reuse
+  __shared__ float fin_sc[(kWin || TRU) ? 1 : 28 * 65];
+  static_assert(!kWin || sizeof(lds_win) >= kFinScratch * sizeof(float), "finalize scratch (window)");
+  static_assert(!TRU || sizeof(lds_ext) >= kFinScratch * sizeof(float), "finalize scratch (extremum buffer)");
 
   const int tid = threadIdx.x, lane = tid & 63, wave = wave_id();
   const int W = p.W, H = p.H, HW = H * W;
@@ -1956,16 +1952,27 @@ __global__ __launch_bounds__(kThreads, DPFT_MIN_WAVES) void ic_reduce_kernel(Ite
     for (int k = 0; k < 6; ++k) st_ag(out + R_CMX + k, (float)(e.c[k]));
   }
   // the last workgroup of a pair reduces its records; the one completing the batch solves
-#if DPFT_TAIL_PROF
-  if (threadIdx.x == 0) {
-    const uint32_t tm = (uint32_t)wall_clock64();
-    atomicMin(p.ctrl + 17, tm);
-    atomicMax(p.ctrl + 18, tm);
-    if (kb < 1024) st_ag(p.ctrl + 64 + kb, tm);  // per-workgroup finish (minmax partial area)
-  }
+#if DPFT_TAIL_PROF  // no atomics: a shared min / max word serialises every workgroup's finish
+  if (threadIdx.x == 0 && kb < kTailWG) st_ag(p.ctrl + kCtlTail + kb, (uint32_t)wall_clock64());
 #endif
+  // the batch-last workgroup reduces every pair's records and solves (LDS scratch: the
+  // marching window, else the extremum buffer -- both dead by now)
   if (p.fin_on && block_is_last(p.fin.pair_cnt + b, 1u, (uint32_t)p.nbpp)) {
-    pair_reduce(p.fin, b);
+#if DPFT_TAIL_PROF
+    const uint32_t t_pl = (uint32_t)wall_clock64();
+#endif
+    if constexpr (kWin)
+      pair_reduce2(p.fin, b, reinterpret_cast<float*>(&lds_win[0][0]));
+    else if constexpr (TRU)
+      pair_reduce2(p.fin, b, &lds_ext[0][0]);
+    else
+      pair_reduce2(p.fin, b, fin_sc);
+#if DPFT_TAIL_PROF
+    if (threadIdx.x == 0 && b < kTailPairs) {
+      st_ag(p.ctrl + kCtlTail + kTailWG + 2 * b, t_pl);
+      st_ag(p.ctrl + kCtlTail + kTailWG + 2 * b + 1, (uint32_t)wall_clock64());
+    }
+#endif
     if (block_is_last(p.fin.done_cnt, 1u, (uint32_t)p.B)) {
 #if DPFT_TAIL_PROF
       const uint32_t t19 = (uint32_t)wall_clock64();
@@ -1974,13 +1981,8 @@ __global__ __launch_bounds__(kThreads, DPFT_MIN_WAVES) void ic_reduce_kernel(Ite
 #if DPFT_TAIL_PROF
       __syncthreads();
       if (threadIdx.x == 0) {
-        const uint32_t t20 = (uint32_t)wall_clock64();
-        for (int i = 0; i < 3; ++i) st_ag(p.ctrl + 24 + i, ld_ag(p.ctrl + 16 + i));
-        st_ag(p.ctrl + 27, t19);
-        st_ag(p.ctrl + 28, t20);
-        st_ag(p.ctrl + 16, 0xFFFFFFFFu);
-        st_ag(p.ctrl + 17, 0xFFFFFFFFu);
-        st_ag(p.ctrl + 18, 0u);
+        st_ag(p.ctrl + kCtlTail + kTailWG + 2 * kTailPairs, t19);
+        st_ag(p.ctrl + kCtlTail + kTailWG + 2 * kTailPairs + 1, (uint32_t)wall_clock64());
       }
 #endif
     }
@@ -2130,7 +2132,8 @@ __global__ __launch_bounds__(kThreads) void finalize_kernel(FinParams q) {
 #if DPFT_ABL_SOLVE == 3  // profiling ablation: empty finalize launch
   return;
 #endif
-  pair_reduce(q, blockIdx.x);
+  __shared__ float sc[kFinScratch];
+  pair_reduce2(q, blockIdx.x, sc);
   if (block_is_last(q.done_cnt, 1u, (uint32_t)q.B)) finalize_batch(q);
 }
 
@@ -2145,12 +2148,13 @@ __global__ __launch_bounds__(kThreads) void finalize_kernel(FinParams q) {
 // save); the per-pixel channel sums meet in LDS behind one barrier per unit and
 // each wave accumulates its share of the normal equations (SplitAcc).
 template <int CT, bool TRU, int MODE>
-__global__ __launch_bounds__(kThreads) void ic_split_kernel(IterParams p) {
+__global__ __launch_bounds__(kThreads, 4) void ic_split_kernel(IterParams p) {  // 4 waves per SIMD: <= 128 VGPRs
   constexpr bool NOSIG = MODE == 2;
   static_assert(MODE != 1, "combine_ICP runs on ic_reduce_kernel");
   constexpr int NQ = CT / 4, QW = NQ / 4;
   static_assert(CT % 16 == 0 && QW >= 1, "4 waves x whole channel quads");
   __shared__ float qs[2][4][9][64];
+  static_assert(sizeof(qs) >= kFinScratch * sizeof(float), "finalize scratch (channel sums)");
   __shared__ float lds_ext[TRU ? 14 : 1][64];
   __shared__ float red[kRec];
 
@@ -2300,7 +2304,7 @@ __global__ __launch_bounds__(kThreads) void ic_split_kernel(IterParams p) {
   }
   acc.write_record(wave, lane, lds_ext, red, p.rec + (size_t)kb * kRec);
   if (p.fin_on && block_is_last(p.fin.pair_cnt + b, 1u, (uint32_t)p.nbpp)) {
-    pair_reduce(p.fin, b);
+    pair_reduce2(p.fin, b, &qs[0][0][0][0]);  // LDS scratch: the channel-sum buffers
     if (block_is_last(p.fin.done_cnt, 1u, (uint32_t)p.B)) finalize_batch(p.fin);
   }
 }
@@ -2758,7 +2762,11 @@ IterParams make_params(const DpftLevelDesc& d, const DpftLevelTensors& tt, const
   p.fin_on = 0;
   p.reverse = 0;
   p.skew = kMarchSkew;
-  if (const char* e = getenv("DPFT_DEBUG_SKEW")) p.skew = atoi(e);  // tuning only
+  static const int skew_env = [] {  // tuning only; read once, clamped: band weights 64 -/+ skew stay positive
+    const char* e = getenv("DPFT_DEBUG_SKEW");
+    return e ? std::min(std::max(atoi(e), 0), 63) : -1;
+  }();
+  if (skew_env >= 0) p.skew = skew_env;
   memset(&p.fin, 0, sizeof(p.fin));
   p.fin.rec = p.rec;
   p.fin.prec = reinterpret_cast<double*>(static_cast<char*>(ws) + kCtrlBytes);

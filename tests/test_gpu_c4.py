@@ -233,6 +233,46 @@ def test_c4_schedules_random(schedule, C, H, W, no_unc, masks):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("reverse", [False, True])
+@pytest.mark.parametrize("C,H,W,masks", [(32, 45, 131, True), (16, 64, 70, False), (32, 120, 160, False)])
+def test_c4_combine_icp_march(C, H, W, masks, reverse):
+    """combine_ICP (MODE 1) on the channel-quad marching path (C = 16 / 32: the ring, the
+    tap cache and the per-pixel ICP term of ic_reduce_kernel<..., true>), forward and
+    reverse marching order, against the NCHW kernel on the same inputs."""
+    from deep_prob_feature_track_amd import ic
+    dev = _dev()
+    g = torch.Generator().manual_seed(C * 7 + H)
+    B = 2
+    f0 = torch.rand(B, C, H, W, generator=g)
+    f1 = torch.roll(f0, shifts=(1, 1), dims=(2, 3)) + 0.01 * torch.rand(B, C, H, W, generator=g)
+    s0 = 0.5 + torch.rand(B, 1, H, W, generator=g)
+    s1 = 0.5 + torch.rand(B, 1, H, W, generator=g)
+    yy, xx = torch.meshgrid(torch.arange(H, dtype=torch.float32), torch.arange(W, dtype=torch.float32), indexing="ij")
+    dep0 = (1.5 + 0.3 * torch.sin(xx / 7.0) + 0.2 * torch.cos(yy / 5.0)).expand(B, 1, H, W).contiguous()
+    dep1 = torch.roll(dep0, shifts=(1, 1), dims=(2, 3)) + 0.001 * torch.rand(B, 1, H, W, generator=g)
+    d0, d1 = 1.0 / dep0, 1.0 / dep1
+    m0 = torch.rand(B, 1, H, W, generator=g) > 0.1
+    m1 = torch.rand(B, 1, H, W, generator=g) > 0.2
+    K = torch.tensor([[W * 0.8, W * 0.8, (W - 1) / 2, (H - 1) / 2]]).repeat(B, 1)
+    f0, f1, s0, s1, d0, d1, dep0, dep1, m0, m1, K = [
+        v.to(dev) for v in (f0, f1, s0, s1, d0, d1, dep0, dep1, m0, m1, K)]
+    R = torch.eye(3, device=dev).repeat(B, 1, 1)
+    R[:, 0, 1], R[:, 1, 0] = 0.01, -0.01
+    t = torch.full((B, 3, 1), 0.003, device=dev)
+    kw = dict(remove_tru_sigma=True, combine_icp=True, depth0=dep0, depth1=dep1, icp_weight=0.01)
+    if masks:
+        kw.update(obj_mask0=m0, obj_mask1=m1)
+    a = ic.iterate((R, t), f0, f1, d0, d1, K, s0, s1, first=True, reverse=reverse, **kw)
+    b = ic.iterate((R, t), ic.pack_features(f0), ic.pack_features(f1), d0, d1, K, s0, s1, first=True,
+                   reverse=reverse, schedule="march", **kw)
+    assert torch.equal(a[4], b[4])  # invalid counts
+    torch.testing.assert_close(b[2], a[2], rtol=2e-6, atol=1e-6 * a[2].abs().max().item())
+    torch.testing.assert_close(b[3], a[3], rtol=1e-4, atol=1e-5 * a[3].abs().max().item())
+    torch.testing.assert_close(b[0], a[0], rtol=0, atol=2e-5)
+    torch.testing.assert_close(b[1], a[1], rtol=0, atol=2e-5)
+
+
+@pytest.mark.gpu
 @pytest.mark.parametrize("packed", [False, True])
 def test_pyramid_solver_extrema_prepass_bit_identical(packed):
     """PyramidSolver's one-launch sigma0 extrema pre-pass (per-level workspace slots,

@@ -55,23 +55,26 @@ for level in ([a.level] if a.level >= 0 else range(len(solver.calls))):
     torch.cuda.synchronize()
     us = e0.elapsed_time(e1) / (a.reps * per) * 1e3
     gbs = solver.algorithmic_bytes(level) / (us * 1e-6) / 1e9
-    if a.tail:
-        w = solver.ws[:29 * 4].view(torch.int32).cpu().numpy().astype("int64") & 0xFFFFFFFF
-        t0 = w[24]
-        print("  tail (us from first WG start): first WG done %.1f, last WG done %.1f, pairs reduced %.1f, "
-              "batch solved %.1f" % tuple((w[i] - t0) / 100.0 for i in (25, 26, 27, 28)))
+    if a.tail:  # DPFT_TAIL_PROF build: ctrl words kCtlTail.. (dpft_ic.hip)
+        import numpy as np
+        CT, NWG, NP = 3264, 768, 16
+        w = solver.ws[:(CT + NWG + 2 * NP + 5) * 4].view(torch.int32).cpu().numpy().astype("int64") & 0xFFFFFFFF
         nb = int(c.desc.B)
         g = int(os.environ.get("DPFT_TAIL_GRID", "512"))
-        import numpy as np
-        f = (solver.ws[:(64 + g) * 4].view(torch.int32).cpu().numpy().astype("int64")[64:] & 0xFFFFFFFF)
+        f = w[CT:CT + g]
+        t0 = f.min()
         f = (f - t0) / 100.0
-        st = (solver.ws[:(64 + 512 + g) * 4].view(torch.int32).cpu().numpy().astype("int64")[64 + 512:] & 0xFFFFFFFF)
-        np.save(os.path.join(ROOT, "gpurun_out", f"tails_l{level}_{a.mode}.npy"), (st - t0) / 100.0)
-        import numpy as np
+        bs = (w[CT + NWG + 2 * NP:CT + NWG + 2 * NP + 2] - t0) / 100.0
+        pr = (w[CT + NWG:CT + NWG + 2 * nb].reshape(nb, 2) - t0) / 100.0
+        sub = (w[CT + NWG + 2 * NP + 2:CT + NWG + 2 * NP + 5] - t0) / 100.0
+        print("  pair 0 reduce: records loaded %.1f, extrema %.1f, trees %.1f" % tuple(sub))
         np.save(os.path.join(ROOT, "gpurun_out", f"tail_l{level}_{a.mode}.npy"), f)
+        print("  timeline (us from the first workgroup finish): last workgroup done %.1f, batch-last detected %.1f, "
+              "batch solved %.1f" % (f.max(), bs[0], bs[1]))
         per = g // nb
         for b in range(nb):
             x = f[b * per:(b + 1) * per]
-            print("   pair %d: finish min %.1f  median %.1f  max %.1f" % (b, x.min(), np.median(x), x.max()))
+            print("   pair %d: finish min %.1f  median %.1f  max %.1f | pair-last detected %.1f, pair reduced %.1f"
+                  % (b, x.min(), np.median(x), x.max(), pr[b, 0], pr[b, 1]))
     print(f"{os.path.basename(os.environ.get('DPFT_LIB', 'libdpft_ic.so'))}{' c4' if a.c4 else ''}{' ' + a.schedule if a.schedule else ''} {a.mode} level {level} B={a.batch}: "
           f"{us:.1f} us/launch, {gbs:.0f} GB/s algorithmic ({gbs / 80:.1f}% of 8 TB/s)", flush=True)
