@@ -750,6 +750,24 @@ __device__ void global_extrema(const float* rec, int nblocks, int imn, int imx, 
   gmax = fmaxf(fmaxf(sm[1][0], sm[1][1]), fmaxf(sm[1][2], sm[1][3]));
 }
 
+// 1 / sqrt(x) in fp64: the hardware estimate plus two Newton steps (the estimate is good
+// to ~2^-22, each step doubles the bits) -- a few dependent FMAs instead of the
+// correctly rounded sqrt and divide sequences on the finalize's serial path.  x = 0 and
+// x < 0 (a non-SPD pivot) give inf / NaN like 1 / sqrt(x).
+#ifndef DPFT_FIN_RSQ
+#define DPFT_FIN_RSQ 1
+#endif
+__device__ __forceinline__ double rsqrt_d(double x) {
+#if !DPFT_FIN_RSQ
+  return 1.0 / sqrt(x);
+#endif
+  double r = __builtin_amdgcn_rsq(x);
+  if (!(x > 0.0) || isinf(x)) return r;
+#pragma unroll
+  for (int i = 0; i < 2; ++i) r = r * __builtin_fma(-0.5 * x * r, r, 1.5);
+  return r;
+}
+
 // Solve (JtJ + 1e-6 tr(JtJ) I) xi = JtR in fp64 (algorithms.py:2094-2103: the
 // damped matrix is SPD, so a fully unrolled register Cholesky replaces the
 // reference's batched inverse) and apply the inverse-compositional update
@@ -778,8 +796,7 @@ __device__ void solve_and_update(const double* jtj_u, const double* jtr, float* 
     double dj = A[j][j];
 #pragma unroll
     for (int m = 0; m < j; ++m) dj -= L[j][m] * L[j][m];
-    const double ljj = sqrt(dj);
-    invd[j] = 1.0 / ljj;
+    invd[j] = rsqrt_d(dj);  // 1 / L[j][j]
 #pragma unroll
     for (int i = j + 1; i < 6; ++i) {
       double v = A[i][j];
@@ -805,8 +822,10 @@ __device__ void solve_and_update(const double* jtj_u, const double* jtr, float* 
   }
   // dR = Exp(-w): Rodrigues, NaN at |w| = 0 exactly as the reference.
   const double w0 = -xi[0], w1 = -xi[1], w2 = -xi[2];
-  const double th = sqrt(w0 * w0 + w1 * w1 + w2 * w2);
-  const double k0 = w0 / th, k1 = w1 / th, k2 = w2 / th;
+  const double th2 = w0 * w0 + w1 * w1 + w2 * w2;
+  const double ith = rsqrt_d(th2);  // inf at |w| = 0: k = NaN, as the reference's w / |w|
+  const double th = th2 * ith;
+  const double k0 = w0 * ith, k1 = w1 * ith, k2 = w2 * ith;
   const double Kx[9] = {0.0, -k2, k1, k2, 0.0, -k0, -k1, k0, 0.0};
   double sn, cs;
 #if DPFT_ABL_SOLVE == 2  // profiling ablation: fp32 trig
@@ -917,6 +936,8 @@ __device__ void finalize_batch_from(const FinParams& q, Get get) {
     solve_and_update(sv, sv + 21, q.R + 9 * b, q.t + 3 * b);
   }
 }
+// (Loading each pair record in one burst of 16-byte sc1 loads before the extrema are
+// known measured 6 us SLOWER per finalize than these field loads: not adopted.)
 __device__ void finalize_batch(const FinParams& q) {
   finalize_batch_from(q, [&](int b, int i) { return ld_ag(q.prec + (size_t)b * kPRec + i); });
 }
@@ -2303,7 +2324,7 @@ __global__ __launch_bounds__(kThreads, 4) void ic_split_kernel(IterParams p) {  
     }
   }
   acc.write_record(wave, lane, lds_ext, red, p.rec + (size_t)kb * kRec);
-  if (p.fin_on && block_is_last(p.fin.pair_cnt + b, 1u, (uint32_t)p.nbpp)) {
+  if (!kSplitSepFin && p.fin_on && block_is_last(p.fin.pair_cnt + b, 1u, (uint32_t)p.nbpp)) {
     pair_reduce2(p.fin, b, &qs[0][0][0][0]);  // LDS scratch: the channel-sum buffers
     if (block_is_last(p.fin.done_cnt, 1u, (uint32_t)p.B)) finalize_batch(p.fin);
   }

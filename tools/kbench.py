@@ -21,6 +21,8 @@ p.add_argument("--mode", choices=["reduce", "iterate", "level"], default="reduce
 p.add_argument("--c4", action="store_true", help="channel-quad packed features")
 p.add_argument("--schedule", default=None, help="auto | march | split (channel-quad reduce kernel)")
 p.add_argument("--tail", action="store_true", help="print the launch timeline of a DPFT_TAIL_PROF build")
+p.add_argument("--from-solve", action="store_true",
+               help="start from the poses of one full pyramid solve (the bench's operating point) instead of identity")
 a = p.parse_args()
 dev = torch.device("cuda:0")
 sel, levels, K = bench.make_inputs(a.batch, 0, dev)
@@ -32,6 +34,9 @@ R = torch.eye(3, device=dev).repeat(a.batch, 1, 1).contiguous()
 t = torch.zeros(a.batch, 3, device=dev)
 import ctypes
 from deep_prob_feature_track_amd import _native as N
+if a.from_solve:
+    solver.run(R, t)
+    torch.cuda.synchronize()
 solver.prepare_extrema()  # per-level sigma0 extrema slots (the levels run with EXTREMA_READY)
 for level in ([a.level] if a.level >= 0 else range(len(solver.calls))):
     c = solver.calls[level]
