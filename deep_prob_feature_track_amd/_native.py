@@ -41,7 +41,7 @@ class LevelTensors(ctypes.Structure):
     ]
 
 
-EXPORTS = ("dpft_workspace_size", "dpft_ic_solve_level", "dpft_ic_iterate", "dpft_ic_residual_level",
+EXPORTS = ("dpft_workspace_size", "dpft_ic_solve_level", "dpft_ic_solve_pyramid", "dpft_ic_iterate", "dpft_ic_residual_level",
            "dpft_residual_poses_workspace_size", "dpft_ic_residual_poses",
            "dpft_ic_reduce_only", "dpft_ic_debug_pixels", "dpft_preprocess_workspace_size",
            "dpft_preprocess_depth", "dpft_pack_features", "dpft_sigma_extrema_levels", "dpft_version",
@@ -64,6 +64,8 @@ def lib():
     L.dpft_workspace_size.restype = sz
     L.dpft_ic_solve_level.argtypes = [P(LevelDesc), P(LevelTensors), vp, vp, vp, vp, vp, sz, vp]
     L.dpft_ic_solve_level.restype = ctypes.c_int
+    L.dpft_ic_solve_pyramid.argtypes = [P(LevelDesc), P(LevelTensors), ctypes.c_int32, vp, vp, vp, sz, vp]
+    L.dpft_ic_solve_pyramid.restype = ctypes.c_int
     L.dpft_ic_iterate.argtypes = [P(LevelDesc), P(LevelTensors), vp, vp, vp, vp, vp, ctypes.c_int, vp, sz, vp]
     L.dpft_ic_iterate.restype = ctypes.c_int
     L.dpft_ic_residual_level.argtypes = [P(LevelDesc), P(LevelTensors), vp, vp, vp, vp, sz, vp]

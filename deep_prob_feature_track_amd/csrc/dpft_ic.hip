@@ -938,8 +938,23 @@ __device__ void finalize_batch_from(const FinParams& q, Get get) {
 }
 // (Loading each pair record in one burst of 16-byte sc1 loads before the extrema are
 // known measured 6 us SLOWER per finalize than these field loads: not adopted.)
+#ifndef DPFT_FIN_BURST8
+#define DPFT_FIN_BURST8 1
+#endif
 __device__ void finalize_batch(const FinParams& q) {
-  finalize_batch_from(q, [&](int b, int i) { return ld_ag(q.prec + (size_t)b * kPRec + i); });
+  if (!DPFT_FIN_BURST8 || q.B > kThreads) {
+    finalize_batch_from(q, [&](int b, int i) { return ld_ag(q.prec + (size_t)b * kPRec + i); });
+    return;
+  }
+  // thread b: every field of pair b's record up front (independent 8-byte sc1 loads, one
+  // round trip), then the same computation from registers
+  double r[46];
+  if ((int)threadIdx.x < q.B) {
+    const double* pr = q.prec + (size_t)threadIdx.x * kPRec;
+#pragma unroll
+    for (int i = 0; i < 46; ++i) r[i] = ld_ag(pr + i);
+  }
+  finalize_batch_from(q, [&](int, int i) { return r[i]; });
 }
 
 // Wave min / max trees (fixed order), every value moved before each step's wait.
@@ -2168,21 +2183,15 @@ __global__ __launch_bounds__(kThreads) void finalize_kernel(FinParams q) {
 // taps / sigma terms are recomputed by each wave (cheap next to the latency they
 // save); the per-pixel channel sums meet in LDS behind one barrier per unit and
 // each wave accumulates its share of the normal equations (SplitAcc).
+// One pass of the channel-split schedule over pair b's units jb, jb + stride, ...:
+// the workgroup's record goes to `out`.
 template <int CT, bool TRU, int MODE>
-__global__ __launch_bounds__(kThreads, 4) void ic_split_kernel(IterParams p) {  // 4 waves per SIMD: <= 128 VGPRs
+__device__ __forceinline__ void split_pass(const IterParams& p, int b, int jb, int stride, float (&qs)[2][4][9][64],
+                                           float (*lds_ext)[64], float* red, float* out) {
   constexpr bool NOSIG = MODE == 2;
-  static_assert(MODE != 1, "combine_ICP runs on ic_reduce_kernel");
   constexpr int NQ = CT / 4, QW = NQ / 4;
-  static_assert(CT % 16 == 0 && QW >= 1, "4 waves x whole channel quads");
-  __shared__ float qs[2][4][9][64];
-  static_assert(sizeof(qs) >= kFinScratch * sizeof(float), "finalize scratch (channel sums)");
-  __shared__ float lds_ext[TRU ? 14 : 1][64];
-  __shared__ float red[kRec];
-
   const int lane = threadIdx.x & 63, wave = wave_id();
   const int W = p.W, H = p.H, HW = H * W;
-  const int kb = xcd_remap(blockIdx.x, gridDim.x);
-  const int b = kb / p.nbpp, jb = kb - b * p.nbpp;
   const int U = p.tiles_x * H;
   const float g0min = TRU ? dec_ord(p.ext[0]) : 0.f, g0max = TRU ? dec_ord(p.ext[1]) : 0.f;
   const uint32_t planeB = (uint32_t)HW * 4u;
@@ -2219,15 +2228,15 @@ __global__ __launch_bounds__(kThreads, 4) void ic_split_kernel(IterParams p) {  
     dnext = bld(rd0, y * W * 4 + xc * 4, 0);
   }
   int par = 0;
-  for (int u = jb; u < U; u += p.nbpp, par ^= 1) {
+  for (int u = jb; u < U; u += stride, par ^= 1) {
     int xc, y;
     bool out_lane;
     unit_xy(u, xc, y, out_lane);
     const float d = dnext;
-    if (u + p.nbpp < U) {
+    if (u + stride < U) {
       int xn, yn;
       bool oln;
-      unit_xy(u + p.nbpp, xn, yn, oln);
+      unit_xy(u + stride, xn, yn, oln);
       dnext = bld(rd0, yn * W * 4 + xn * 4, 0);
     }
     const Warp fw = warp_point(xc, y, d, Rm, tv, fx, fy, cx, cy);
@@ -2323,7 +2332,23 @@ __global__ __launch_bounds__(kThreads, 4) void ic_split_kernel(IterParams p) {  
       acc.add(wave, lane, Saa, Sab, Sbb, Sa, Sb, Sar, Sbr, Jx, Jy, invalid, sr0, lds_ext);
     }
   }
-  acc.write_record(wave, lane, lds_ext, red, p.rec + (size_t)kb * kRec);
+  acc.write_record(wave, lane, lds_ext, red, out);
+}
+
+template <int CT, bool TRU, int MODE>
+__global__ __launch_bounds__(kThreads, 4) void ic_split_kernel(IterParams p) {  // 4 waves per SIMD: <= 128 VGPRs
+  constexpr bool NOSIG = MODE == 2;
+  static_assert(MODE != 1, "combine_ICP runs on ic_reduce_kernel");
+  constexpr int NQ = CT / 4, QW = NQ / 4;
+  static_assert(CT % 16 == 0 && QW >= 1, "4 waves x whole channel quads");
+  __shared__ float qs[2][4][9][64];
+  static_assert(sizeof(qs) >= kFinScratch * sizeof(float), "finalize scratch (channel sums)");
+  __shared__ float lds_ext[TRU ? 14 : 1][64];
+  __shared__ float red[kRec];
+  const int kb = xcd_remap(blockIdx.x, gridDim.x);
+  const int b = kb / p.nbpp, jb = kb - b * p.nbpp;
+  split_pass<CT, TRU, MODE>(p, b, jb, p.nbpp, qs, lds_ext, red, p.rec + (size_t)kb * kRec);
+
   if (!kSplitSepFin && p.fin_on && block_is_last(p.fin.pair_cnt + b, 1u, (uint32_t)p.nbpp)) {
     pair_reduce2(p.fin, b, &qs[0][0][0][0]);  // LDS scratch: the channel-sum buffers
     if (block_is_last(p.fin.done_cnt, 1u, (uint32_t)p.B)) finalize_batch(p.fin);
@@ -2975,6 +3000,52 @@ int iterate_impl(const DpftLevelDesc* desc, const DpftLevelTensors* tt, float* R
   return launch_reduce(p, st);
 }
 
+int solve_level_impl(const DpftLevelDesc* desc, const DpftLevelTensors* tensors, float* R, float* t, float* jtj_out,
+                     float* jtr_out, void* ws, size_t ws_bytes, hipStream_t st) {
+  int rc = check_desc(desc);
+  if (rc) return rc;
+  for (int it = 0; it < desc->iters; ++it) {
+    const bool last = it == desc->iters - 1;
+    const int flags = (it == 0 ? DPFT_ITER_FIRST : 0) | ((it & 1) ? DPFT_ITER_REVERSE : 0);
+    rc = iterate_impl(desc, tensors, R, t, last ? jtj_out : nullptr, last ? jtr_out : nullptr, nullptr, flags, ws,
+                      ws_bytes, st);
+    if (rc) return rc;
+  }
+  return DPFT_OK;
+}
+
+int sigma_extrema_impl(const DpftLevelDesc* descs, const DpftLevelTensors* tensors, int levels, void* workspace,
+                       size_t workspace_bytes, hipStream_t st);
+
+int pyramid_impl(const DpftLevelDesc* descs, const DpftLevelTensors* tt, int levels, float* R, float* t, void* ws,
+                 size_t ws_bytes, hipStream_t st) {
+  if (!descs || !tt || !R || !t || !ws) return fail(DPFT_E_INVALID, "null pointer");
+  if (levels < 1 || levels > 8) return fail(DPFT_E_INVALID, "levels=%d outside [1, 8]", levels);
+  int rc;
+  for (int l = 0; l < levels; ++l) {
+    if ((rc = check_desc(&descs[l]))) return rc;
+    if ((rc = check_tensors(&tt[l], descs[l].flags))) return rc;
+    if (ws_bytes < ws_need(descs[l])) return fail(DPFT_E_WORKSPACE, "workspace %zu < %zu", ws_bytes, ws_need(descs[l]));
+    const DpftLevelDesc& a = descs[0];
+    const DpftLevelDesc& d = descs[l];
+    const uint32_t same = ~(DPFT_EXT_SLOT_MASK | DPFT_EXTREMA_READY | DPFT_SCHED_MASK);
+    if (d.B != a.B || d.C != a.C || d.Cs != a.Cs || d.iters != a.iters || (d.flags & same) != (a.flags & same))
+      return fail(DPFT_E_INVALID, "level %d: B / C / Cs / iters / flags differ from level 0 of the call", l);
+    if ((d.flags & DPFT_REMOVE_TRU_SIGMA) && !(d.flags & DPFT_EXT_SLOT_MASK))
+      return fail(DPFT_E_INVALID, "level %d: REMOVE_TRU_SIGMA needs DPFT_EXT_SLOT (one extrema pre-pass)", l);
+  }
+  // one pose-independent pre-pass for every level's sigma0 extrema, then the levels
+  std::vector<DpftLevelDesc> d(descs, descs + levels);
+  if (d[0].flags & DPFT_REMOVE_TRU_SIGMA) {
+    if (levels > 4) return fail(DPFT_E_INVALID, "truncated sigma: at most 4 levels per pre-pass");
+    for (auto& x : d) x.flags |= DPFT_EXTREMA_READY;
+    if ((rc = sigma_extrema_impl(d.data(), tt, levels, ws, ws_bytes, st))) return rc;
+  }
+  for (int l = 0; l < levels; ++l)
+    if ((rc = solve_level_impl(&d[l], &tt[l], R, t, nullptr, nullptr, ws, ws_bytes, st))) return rc;
+  return DPFT_OK;
+}
+
 int residual_impl(const DpftLevelDesc* desc, const DpftLevelTensors* tt, int P, const float* R, const float* t,
                   float* loss, void* ws, size_t ws_bytes, hipStream_t st) {
   int rc = check_desc(desc);
@@ -3024,16 +3095,13 @@ int dpft_ic_iterate(const DpftLevelDesc* desc, const DpftLevelTensors* tensors, 
 
 int dpft_ic_solve_level(const DpftLevelDesc* desc, const DpftLevelTensors* tensors, float* R, float* t,
                         float* jtj_out, float* jtr_out, void* workspace, size_t workspace_bytes, void* hip_stream) {
-  int rc = check_desc(desc);
-  if (rc) return rc;
-  for (int it = 0; it < desc->iters; ++it) {
-    const bool last = it == desc->iters - 1;
-    const int flags = (it == 0 ? DPFT_ITER_FIRST : 0) | ((it & 1) ? DPFT_ITER_REVERSE : 0);
-    rc = iterate_impl(desc, tensors, R, t, last ? jtj_out : nullptr, last ? jtr_out : nullptr, nullptr, flags,
-                      workspace, workspace_bytes, static_cast<hipStream_t>(hip_stream));
-    if (rc) return rc;
-  }
-  return DPFT_OK;
+  return solve_level_impl(desc, tensors, R, t, jtj_out, jtr_out, workspace, workspace_bytes,
+                          static_cast<hipStream_t>(hip_stream));
+}
+
+int dpft_ic_solve_pyramid(const DpftLevelDesc* descs, const DpftLevelTensors* tensors, int32_t levels, float* R,
+                          float* t, void* workspace, size_t workspace_bytes, void* hip_stream) {
+  return pyramid_impl(descs, tensors, levels, R, t, workspace, workspace_bytes, static_cast<hipStream_t>(hip_stream));
 }
 
 int dpft_ic_residual_level(const DpftLevelDesc* desc, const DpftLevelTensors* tt, const float* R, const float* t,
@@ -3077,6 +3145,13 @@ int dpft_ic_debug_pixels(const DpftLevelDesc* desc, const DpftLevelTensors* tt, 
 
 int dpft_sigma_extrema_levels(const DpftLevelDesc* descs, const DpftLevelTensors* tensors, int32_t levels,
                               void* workspace, size_t workspace_bytes, void* hip_stream) {
+  return sigma_extrema_impl(descs, tensors, levels, workspace, workspace_bytes, static_cast<hipStream_t>(hip_stream));
+}
+}  // extern "C"
+
+namespace {
+int sigma_extrema_impl(const DpftLevelDesc* descs, const DpftLevelTensors* tensors, int levels, void* workspace,
+                       size_t workspace_bytes, hipStream_t st) {
   if (!descs || !tensors || !workspace) return fail(DPFT_E_INVALID, "null pointer");
   if (levels < 1 || levels > 4) return fail(DPFT_E_INVALID, "levels=%d outside [1, 4]", levels);
   MMLevels a;
@@ -3101,10 +3176,13 @@ int dpft_sigma_extrema_levels(const DpftLevelDesc* descs, const DpftLevelTensors
   }
   const int grid = (int)std::min<size_t>((nmax + kThreads * 16 - 1) / (kThreads * 16), kMMGrid);
   static_assert(4 * 2 * kMMGrid <= 2 * kMaxMMBlocks, "per-level minmax partials");
-  hipLaunchKernelGGL(minmax_levels_kernel, dim3(grid, levels), dim3(kThreads), 0, static_cast<hipStream_t>(hip_stream), a,
+  hipLaunchKernelGGL(minmax_levels_kernel, dim3(grid, levels), dim3(kThreads), 0, st, a,
                      static_cast<uint32_t*>(workspace));
   return hip_check("minmax_levels_kernel");
 }
+}  // namespace
+
+extern "C" {
 
 size_t dpft_preprocess_workspace_size(void) { return kCtrlBytes; }
 

@@ -11,6 +11,7 @@ Reference counterparts: `TrustRegionInverseWUncertainty.forward` /
 `forward_residuals` (code/models/algorithms.py:611-786).
 """
 import ctypes
+import os
 
 import torch
 
@@ -305,6 +306,7 @@ class PyramidSolver:
         # sigma): each level keeps them in its own workspace slot and skips the
         # per-level min/max launch (dpft_sigma_extrema_levels, DPFT_EXTREMA_READY).
         # Not with combine_icp (its depth1 pass shares the min/max scratch words).
+        self.remove_tru_sigma = bool(remove_tru_sigma)
         self.extrema_prepass = bool(remove_tru_sigma) and not combine_icp and len(self.calls) <= 4
         if self.extrema_prepass:
             for l, c in enumerate(self.calls):
@@ -324,10 +326,25 @@ class PyramidSolver:
                                                    self.ws_bytes, _stream(self.device))
             N.check(rc, "dpft_sigma_extrema_levels")
 
-    def run(self, R, t):
-        """In place: R [B,3,3], t [B,3] fp32 contiguous device buffers."""
+    def run(self, R, t, per_level=None):
+        """In place: R [B,3,3], t [B,3] fp32 contiguous device buffers.
+
+        One dpft_ic_solve_pyramid call (the sigma0 extrema pre-pass, then every level),
+        or with per_level=True the same launches from one dpft_ic_solve_level call per
+        level (tests check the two are bit-identical)."""
+        if per_level is None:  # A/B knob for tuning runs only
+            per_level = os.environ.get("DPFT_PER_LEVEL", "0") == "1"
         L = N.lib()
         st = _stream(self.device)
+        # (truncated sigma without the one-launch extrema pre-pass -- combine_icp -- keeps
+        # the per-level minmax passes)
+        if not per_level and (self.extrema_prepass or not self.remove_tru_sigma):
+            n = len(self.calls)
+            descs = (N.LevelDesc * n)(*[c.desc for c in reversed(self.calls)])
+            tens = (N.LevelTensors * n)(*[c.tens for c in reversed(self.calls)])
+            rc = L.dpft_ic_solve_pyramid(descs, tens, n, _ptr(R), _ptr(t), _ptr(self.ws), self.ws_bytes, st)
+            N.check(rc, "dpft_ic_solve_pyramid")
+            return
         self.prepare_extrema()
         for c in reversed(self.calls):
             rc = L.dpft_ic_solve_level(ctypes.byref(c.desc), ctypes.byref(c.tens), _ptr(R), _ptr(t), None, None,

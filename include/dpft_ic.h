@@ -18,6 +18,8 @@
  *                                compute_jtj / compute_jtr 812-834,
  *                                GN_solver -> lev_mar_H -> inverse_update_pose
  *                                836-846, 2094-2103, 2035-2054)
+ *   dpft_ic_solve_pyramid  <- the coarse-to-fine level loop of LeastSquareTracking.forward
+ *                             code/models/LeastSquareTracking.py:349-445 (tr_update3..0)
  *   dpft_ic_iterate        <- ONE pass of the loop body algorithms.py:646-693
  *   dpft_ic_residual_level <- TrustRegionInverseWUncertainty.forward_residuals
  *                             algorithms.py:725-786 (+ compute_avg_loss 2119-2137)
@@ -132,6 +134,18 @@ size_t dpft_workspace_size(const DpftLevelDesc* desc);
 int dpft_ic_solve_level(const DpftLevelDesc* desc, const DpftLevelTensors* tensors,
                         float* R, float* t, float* jtj_out, float* jtr_out,
                         void* workspace, size_t workspace_bytes, void* hip_stream);
+
+/*
+ * A whole coarse-to-fine solve: descs[0] / tensors[0] is the COARSEST level, the last
+ * one level 0 (LeastSquareTracking.forward runs tr_update3 .. tr_update0,
+ * LeastSquareTracking.py:349-445), each desc->iters iterations, R / t chained in place.
+ * All levels share B, C, Cs, iters and flags (their K already divided by 2^level) and
+ * one workspace of the largest level's size.  With DPFT_REMOVE_TRU_SIGMA every desc
+ * carries DPFT_EXT_SLOT (<= 4 levels): the sigma0 extrema of all levels come from one
+ * pre-pass (dpft_sigma_extrema_levels), then each level runs as dpft_ic_solve_level.
+ */
+int dpft_ic_solve_pyramid(const DpftLevelDesc* descs, const DpftLevelTensors* tensors, int32_t levels,
+                          float* R, float* t, void* workspace, size_t workspace_bytes, void* hip_stream);
 
 /*
  * One iteration (residual -> Jacobian -> JtJ/JtR -> damped solve -> update).

@@ -290,7 +290,7 @@ def test_pyramid_solver_extrema_prepass_bit_identical(packed):
     solver = ic.PyramidSolver(levels, K, iters=3, remove_tru_sigma=True)
     assert solver.extrema_prepass
     R, t = R0.clone().contiguous(), t0.reshape(-1, 3).clone().contiguous()
-    solver.run(R, t)
+    solver.run(R, t, per_level=True)
     Rs, ts = R0.clone(), t0.reshape(-1, 3, 1).clone()
     for l in reversed(range(len(levels))):
         d = levels[l]
@@ -300,6 +300,42 @@ def test_pyramid_solver_extrema_prepass_bit_identical(packed):
     assert torch.equal(R, Rs) and torch.equal(t, ts.reshape(-1, 3))
     for prec in ("f32", "f64"):
         assert np.abs(R.cpu().numpy() - z[f"{prec}_R"][-1]).max() <= SE3_TOL
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("no_unc", [False, True])
+@pytest.mark.parametrize("B", [1, 8])
+def test_pyramid_entry_point(B, no_unc):
+    """dpft_ic_solve_pyramid (the level loop of LeastSquareTracking.forward in one C call)
+    against one dpft_ic_solve_level call per level: the same launches, bit for bit, and
+    on the golden case the reference's own poses.  B = 8: the bench's batch (replicated
+    golden pair); B = 1."""
+    from deep_prob_feature_track_amd import ic
+    dev = _dev()
+    case, z = golden_io.load("cfg2_640x480_c32")
+    lv = golden_io.levels_torch(case, torch.float32, dev)
+    R0, t0 = golden_io.init_pose(case, torch.float32, dev)
+    K = torch.from_numpy(case["K"]).to(dev)
+    rep = lambda x: x.repeat(B, *([1] * (x.dim() - 1)))
+    levels = [dict(x0=rep(ic.pack_features(d["f0"])), x1=rep(ic.pack_features(d["f1"])), invD0=rep(d["invD0"]),
+                   invD1=rep(d["invD1"]), sigma0=rep(d["s0"]), sigma1=rep(d["s1"])) for d in lv]
+    solver = ic.PyramidSolver(levels, rep(K), iters=3, remove_tru_sigma=not no_unc)
+    if no_unc:
+        for c in solver.calls:
+            c.desc.flags |= ic.N.NO_UNCERTAINTY
+    outs = []
+    for per_level in (False, True):
+        R, t = rep(R0).contiguous(), rep(t0.reshape(-1, 3)).contiguous()
+        solver.run(R, t, per_level=per_level)
+        torch.cuda.synchronize()
+        ic.check_status(solver.status)
+        outs.append((R.cpu().numpy(), t.cpu().numpy()))
+    (Ra, ta), (Rb, tb) = outs
+    assert np.array_equal(Ra, Rb) and np.array_equal(ta, tb)
+    if not no_unc:
+        for prec in ("f32", "f64"):
+            assert np.abs(Ra - z[f"{prec}_R"][-1]).max() <= SE3_TOL
+            assert np.abs(ta - z[f"{prec}_t"][-1]).max() <= SE3_TOL
 
 
 @pytest.mark.gpu
