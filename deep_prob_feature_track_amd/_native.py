@@ -13,6 +13,7 @@ import torch  # noqa: F401  (must be imported before the HIP library, see above)
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(_HERE, "libdpft_ic.so")
 
+ITER_FIRST, ITER_REVERSE, ITER_NO_UPDATE = 0x1, 0x2, 0x4
 REMOVE_TRU_SIGMA = 0x1
 COMBINE_ICP = 0x2
 NO_UNCERTAINTY = 0x4
@@ -21,7 +22,7 @@ SCHEDULES = {"auto": 0x00, "march": 0x10, "split": 0x20}  # DPFT_SCHED_*
 EXT_SLOT_SHIFT = 12       # DPFT_EXT_SLOT(k) = (k + 1) << 12
 EXTREMA_READY = 0x10000
 STATUS_NONFINITE = 0x1
-ABI_VERSION = 1
+ABI_VERSION = 2
 
 
 class LevelDesc(ctypes.Structure):
@@ -37,12 +38,12 @@ class LevelTensors(ctypes.Structure):
         ("f0", ctypes.c_void_p), ("f1", ctypes.c_void_p), ("s0", ctypes.c_void_p), ("s1", ctypes.c_void_p),
         ("invD0", ctypes.c_void_p), ("invD1", ctypes.c_void_p), ("depth0", ctypes.c_void_p),
         ("depth1", ctypes.c_void_p), ("mask0", ctypes.c_void_p), ("mask1", ctypes.c_void_p),
-        ("K", ctypes.c_void_p), ("status", ctypes.c_void_p),
+        ("K", ctypes.c_void_p), ("status", ctypes.c_void_p), ("weights", ctypes.c_void_p),
     ]
 
 
 EXPORTS = ("dpft_workspace_size", "dpft_ic_solve_level", "dpft_ic_solve_pyramid", "dpft_ic_iterate", "dpft_ic_residual_level",
-           "dpft_residual_poses_workspace_size", "dpft_ic_residual_poses",
+           "dpft_residual_poses_workspace_size", "dpft_ic_residual_poses", "dpft_ic_residual_map",
            "dpft_ic_reduce_only", "dpft_ic_debug_pixels", "dpft_preprocess_workspace_size",
            "dpft_preprocess_depth", "dpft_pack_features", "dpft_sigma_extrema_levels", "dpft_version",
            "dpft_last_error")
@@ -74,6 +75,8 @@ def lib():
     L.dpft_residual_poses_workspace_size.restype = sz
     L.dpft_ic_residual_poses.argtypes = [P(LevelDesc), P(LevelTensors), ctypes.c_int32, vp, vp, vp, vp, sz, vp]
     L.dpft_ic_residual_poses.restype = ctypes.c_int
+    L.dpft_ic_residual_map.argtypes = [P(LevelDesc), P(LevelTensors), vp, vp, vp, vp, vp, sz, vp]
+    L.dpft_ic_residual_map.restype = ctypes.c_int
     L.dpft_ic_reduce_only.argtypes = [P(LevelDesc), P(LevelTensors), vp, vp, vp, sz, vp]
     L.dpft_ic_reduce_only.restype = ctypes.c_int
     L.dpft_ic_debug_pixels.argtypes = [P(LevelDesc), P(LevelTensors), vp, vp, vp, vp, sz, vp]

@@ -382,6 +382,7 @@ struct FinParams {
   uint32_t* done_cnt; // pairs finished
   int nblocks, per_pair, HW;
   uint32_t flags;
+  int no_update;      // DPFT_ITER_NO_UPDATE: normal equations out, pose unchanged
   float* R;
   float* t;
   float* jtj_out;
@@ -400,6 +401,7 @@ struct IterParams {
   const float* invD1;
   const uint8_t* mask0;
   const uint8_t* mask1;
+  const float* wgt;      // NO_UNCERTAINTY: per-pixel M-estimator weights [B,1,H,W] (nullable)
   const float* depth0;   // COMBINE_ICP: raw depth pyramids level (max-pooled), [B,1,H,W]
   const float* depth1;
   const float* nrm1;     // COMBINE_ICP: normal map of frame 1, [B,3,H,W] (workspace, per level)
@@ -933,7 +935,7 @@ __device__ void finalize_batch_from(const FinParams& q, Get get) {
 #pragma unroll
       for (int k = 0; k < 6; ++k) q.jtr_out[6 * b + k] = (float)sv[21 + k];
     if (q.invalid_out) q.invalid_out[b] = (int32_t)sv[27];
-    solve_and_update(sv, sv + 21, q.R + 9 * b, q.t + 3 * b);
+    if (!q.no_update) solve_and_update(sv, sv + 21, q.R + 9 * b, q.t + 3 * b);
   }
 }
 // (Loading each pair record in one burst of 16-byte sc1 loads before the extrema are
@@ -1306,8 +1308,11 @@ __global__ __launch_bounds__(kThreads, DPFT_MIN_WAVES) void ic_reduce_kernel(Ite
 #pragma unroll
     for (int r = 0; r < R; ++r) {
       if (!F.out_lane || F.y0 + r >= H) continue;
-      const float Sa = -S.Sa[r], Sb = -S.Sb[r], Sar = -S.Sar[r], Sbr = -S.Sbr[r];
-      const float Saa = S.Saa[r], Sab = S.Sab[r], Sbb = S.Sbb[r];
+      // IC tracker with a learned M-estimator: the pixel's weight scales its J^T W J and
+      // J^T W r terms (wJ = weights * J, algorithms.py:71-76; JtR = J^T (weights * r), 1631-1632)
+      const float wp = (NOSIG && p.wgt) ? p.wgt[(size_t)b * HW + (size_t)(F.y0 + r) * W + F.xc] : 1.0f;
+      const float Sa = -S.Sa[r] * wp, Sb = -S.Sb[r] * wp, Sar = -S.Sar[r] * wp, Sbr = -S.Sbr[r] * wp;
+      const float Saa = S.Saa[r] * wp, Sab = S.Sab[r] * wp, Sbb = S.Sbb[r] * wp;
       const bool invalid = T.invalid[r];
       float Jx[6], Jy[6];
       warp_jac(F.wp[r].xr, F.wp[r].yr, F.d[r], fx, fy, Jx, Jy);
@@ -2502,6 +2507,34 @@ __global__ __launch_bounds__(kThreads) void ic_debug_pixels_kernel(IterParams p,
   o[4 * HW] = px.invalid ? 1.0f : 0.0f;
 }
 
+// The IC tracker's residual map at a pose (compute_warped_residual, algorithms.py:1919-1957):
+// r_c = bilinear(f1_c, warp) - f0_c, 1e-3 on occluded / masked pixels, and the occlusion
+// map -- the input of the learned M-estimator (DeepRobustEstimator, 1467-1477) and of
+// its weighted loss.  One thread per pixel, every channel (NCHW or channel-quad f0 / f1).
+__global__ __launch_bounds__(kThreads) void ic_residual_map_kernel(IterParams p, float* out, uint8_t* occ_out) {
+  const int W = p.W, H = p.H, HW = H * W;
+  const long i = (long)blockIdx.x * kThreads + threadIdx.x;
+  if (i >= (long)p.B * HW) return;
+  const int b = (int)(i / HW), pix = (int)(i - (long)b * HW), y = pix / W, x = pix - y * W;
+  const float fx = p.K[4 * b + 0], fy = p.K[4 * b + 1], cx = p.K[4 * b + 2], cy = p.K[4 * b + 3];
+  float Rm[9], tv[3];
+  for (int k = 0; k < 9; ++k) Rm[k] = p.R[9 * b + k];
+  for (int k = 0; k < 3; ++k) tv[k] = p.t[3 * b + k];
+  const float d = p.invD0[(size_t)b * HW + pix];
+  PixelFrame px;
+  setup_pixel(p, b, x, y, d, Rm, tv, fx, fy, cx, cy, px);
+  const bool c4 = (p.flags & DPFT_FEATURES_C4) != 0;
+  const int fs = c4 ? 4 : 1;
+  const float* f0b = p.f0 + (size_t)b * p.C * HW;
+  const float* f1b = p.f1 + (size_t)b * p.C * HW;
+  float* o = out + (size_t)b * p.C * HW + pix;
+  for (int c = 0; c < p.C; ++c) {
+    const float r = bil_s(chan_base(f1b, c, HW, c4), px.tp, fs) - chan_base(f0b, c, HW, c4)[(size_t)pix * fs];
+    o[(size_t)c * HW] = px.invalid ? 1e-3f : r;
+  }
+  if (occ_out) occ_out[i] = px.invalid ? 1 : 0;
+}
+
 // NCHW -> channel-quad layout: thread i = (b, q, pixel) gathers channels 4q..4q+3
 // (four coalesced plane reads) into one 16-byte store.
 __global__ __launch_bounds__(kThreads) void pack_c4_kernel(const float* __restrict__ src, f32x4* __restrict__ dst,
@@ -2735,6 +2768,8 @@ int check_tensors(const DpftLevelTensors* t, uint32_t flags = 0) {
   if (!(flags & DPFT_NO_UNCERTAINTY) && (!t->s0 || !t->s1)) return fail(DPFT_E_INVALID, "null sigma pointer");
   if ((flags & DPFT_COMBINE_ICP) && (!t->depth0 || !t->depth1))
     return fail(DPFT_E_INVALID, "COMBINE_ICP needs depth0 and depth1");
+  if (t->weights && !(flags & DPFT_NO_UNCERTAINTY))
+    return fail(DPFT_E_INVALID, "per-pixel weights are the IC tracker's M-estimator (NO_UNCERTAINTY only)");
   return DPFT_OK;
 }
 
@@ -2778,6 +2813,7 @@ IterParams make_params(const DpftLevelDesc& d, const DpftLevelTensors& tt, const
   p.invD1 = tt.invD1;
   p.mask0 = tt.mask0;
   p.mask1 = tt.mask1;
+  p.wgt = tt.weights;
   p.depth0 = tt.depth0;
   p.depth1 = tt.depth1;
   p.nrm1 = (d.flags & DPFT_COMBINE_ICP) ? reinterpret_cast<const float*>(static_cast<char*>(ws) + nrm_offset(d))
@@ -2941,7 +2977,7 @@ int launch_reduce_c4(const IterParams& p, hipStream_t st) {
     uint32_t sched = p.flags & DPFT_SCHED_MASK;
     if (sched == DPFT_SCHED_AUTO)  // coarse levels (few pixels per pair): the channel-split kernel
       sched = ((long)p.H * p.W <= kSplitMaxPixels) ? DPFT_SCHED_SPLIT : DPFT_SCHED_MARCH;
-    if (!(p.flags & DPFT_COMBINE_ICP)) {  // combine_ICP: ic_reduce_kernel (marching path)
+    if (!(p.flags & DPFT_COMBINE_ICP) && !p.wgt) {  // combine_ICP / M-estimator weights: ic_reduce_kernel
       if (sched == DPFT_SCHED_SPLIT) {
         if (p.flags & DPFT_NO_UNCERTAINTY) return launch_split<CT, false, 2>(p, st);
         return tru ? launch_split<CT, true, 0>(p, st) : launch_split<CT, false, 0>(p, st);
@@ -2992,6 +3028,7 @@ int iterate_impl(const DpftLevelDesc* desc, const DpftLevelTensors* tt, float* R
   IterParams p = make_params(*desc, *tt, g, R, t, ws);
   p.reverse = (first & DPFT_ITER_REVERSE) ? 1 : 0;
   p.fin_on = 1;
+  p.fin.no_update = (first & DPFT_ITER_NO_UPDATE) ? 1 : 0;
   p.fin.R = R;
   p.fin.t = t;
   p.fin.jtj_out = jtj_out;
@@ -3141,6 +3178,22 @@ int dpft_ic_debug_pixels(const DpftLevelDesc* desc, const DpftLevelTensors* tt, 
   hipLaunchKernelGGL(ic_debug_pixels_kernel, dim3((n + kThreads - 1) / kThreads), dim3(kThreads), 0,
                      static_cast<hipStream_t>(hip_stream), p, out);
   return hip_check("ic_debug_pixels_kernel");
+}
+
+int dpft_ic_residual_map(const DpftLevelDesc* desc, const DpftLevelTensors* tt, const float* R, const float* t,
+                         float* out, uint8_t* occ_out, void* ws, size_t ws_bytes, void* hip_stream) {
+  int rc = check_desc(desc);
+  if (rc) return rc;
+  if ((rc = check_tensors(tt, desc->flags))) return rc;
+  if (!(desc->flags & DPFT_NO_UNCERTAINTY))
+    return fail(DPFT_E_INVALID, "the residual map is the IC tracker's (DPFT_NO_UNCERTAINTY)");
+  if (!R || !t || !out || !ws || ws_bytes < ws_need(*desc)) return fail(DPFT_E_INVALID, "null pointer or small workspace");
+  const Geometry g = plan(*desc);
+  const IterParams p = make_params(*desc, *tt, g, R, t, ws);
+  const long n = (long)desc->B * desc->H * desc->W;
+  hipLaunchKernelGGL(ic_residual_map_kernel, dim3((unsigned)((n + kThreads - 1) / kThreads)), dim3(kThreads), 0,
+                     static_cast<hipStream_t>(hip_stream), p, out, occ_out);
+  return hip_check("ic_residual_map_kernel");
 }
 
 int dpft_sigma_extrema_levels(const DpftLevelDesc* descs, const DpftLevelTensors* tensors, int32_t levels,

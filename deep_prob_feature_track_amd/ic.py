@@ -108,7 +108,7 @@ class LevelCall:
 
     def __init__(self, x0, x1, invD0, invD1, K, sigma0, sigma1, iters=3, remove_tru_sigma=False,
                  obj_mask0=None, obj_mask1=None, depth0=None, depth1=None, combine_icp=False,
-                 icp_weight=0.01, status=None, no_uncertainty=False, pack=False, schedule=None):
+                 icp_weight=0.01, status=None, no_uncertainty=False, pack=False, schedule=None, weights=None):
         if not x0.is_cuda:
             raise RuntimeError("the HIP solver needs device tensors (got CPU); there is no CPU fallback")
         for name, t in (("x0", x0), ("x1", x1), ("invD0", invD0), ("invD1", invD1), ("K", K)):
@@ -155,13 +155,20 @@ class LevelCall:
             if depth0 is None or depth1 is None:
                 raise ValueError("combine_icp needs depth0 and depth1")
             flags |= N.COMBINE_ICP
+        if weights is not None:  # IC tracker's M-estimator weights, one per pixel
+            if not no_uncertainty:
+                raise ValueError("per-pixel weights belong to the IC tracker (no_uncertainty=True)")
+            if weights.numel() != B * H * W:
+                raise ValueError(f"weights must hold one value per pixel [B,1,H,W] (got {tuple(weights.shape)})")
+            weights = weights.reshape(B, 1, H, W).to(torch.float32).contiguous()
+        self.w = weights
         self.d0 = depth0.contiguous() if depth0 is not None else None
         self.d1 = depth1.contiguous() if depth1 is not None else None
         self.status = status if status is not None else torch.zeros(1, dtype=torch.int32, device=self.device)
         self.desc = N.LevelDesc(B, C, cs0, H, W, iters, flags, icp_weight)
         self.tens = N.LevelTensors(_ptr(self.x0), _ptr(self.x1), _ptr(self.s0), _ptr(self.s1), _ptr(self.invD0),
                                    _ptr(self.invD1), _ptr(self.d0), _ptr(self.d1), _ptr(self.m0), _ptr(self.m1),
-                                   _ptr(self.K), _ptr(self.status))
+                                   _ptr(self.K), _ptr(self.status), _ptr(self.w))
         self.B = B
         nbytes = N.lib().dpft_workspace_size(ctypes.byref(self.desc))
         if nbytes == 0:
@@ -197,19 +204,36 @@ def solve_level(pose, x0, x1, invD0, invD1, K, sigma0, sigma1, iters=3, return_j
     return out + (jtj,) if return_jtj else out
 
 
-def iterate(pose, x0, x1, invD0, invD1, K, sigma0, sigma1, first=True, reverse=False, **kw):
+def iterate(pose, x0, x1, invD0, invD1, K, sigma0, sigma1, first=True, reverse=False, update=True, **kw):
     """One iteration; returns (R, t [B,3,1], JtJ [B,6,6], JtR [B,6], invalid [B]) -- test / trace API.
-    reverse=True: the marching order of the solve's odd iterations (DPFT_ITER_REVERSE)."""
+    reverse=True: the marching order of the solve's odd iterations (DPFT_ITER_REVERSE).
+    update=False: the normal equations at `pose` only, R / t returned unchanged
+    (DPFT_ITER_NO_UPDATE, the residual-volume samples of 'Direct-ResVol')."""
     c = LevelCall(x0, x1, invD0, invD1, K, sigma0, sigma1, iters=1, **kw)
     R, t = c.pose_buffers(pose)
     jtj = torch.empty(c.B, 6, 6, dtype=torch.float32, device=c.device)
     jtr = torch.empty(c.B, 6, dtype=torch.float32, device=c.device)
     inv = torch.empty(c.B, dtype=torch.int32, device=c.device)
     rc = N.lib().dpft_ic_iterate(ctypes.byref(c.desc), ctypes.byref(c.tens), _ptr(R), _ptr(t), _ptr(jtj), _ptr(jtr),
-                                 _ptr(inv), (1 if first else 0) | (2 if reverse else 0), _ptr(c.ws), c.ws_bytes,
-                                 _stream(c.device))
+                                 _ptr(inv), (N.ITER_FIRST if first else 0) | (N.ITER_REVERSE if reverse else 0) |
+                                 (0 if update else N.ITER_NO_UPDATE), _ptr(c.ws), c.ws_bytes, _stream(c.device))
     N.check(rc, "dpft_ic_iterate")
     return R, t.view(c.B, 3, 1), jtj, jtr, inv
+
+
+def residual_map(pose, x0, x1, invD0, invD1, K, **kw):
+    """IC tracker residuals at `pose` (compute_warped_residual, algorithms.py:1919-1957):
+    (r [B,C,H,W] with 1e-3 on occluded / masked pixels, occ [B,1,H,W] bool)."""
+    kw = dict(kw, no_uncertainty=True)
+    c = LevelCall(x0, x1, invD0, invD1, K, None, None, iters=1, **kw)
+    R, t = c.pose_buffers(pose)
+    B, C, H, W = feature_shape(c.x0)
+    out = torch.empty(B, C, H, W, dtype=torch.float32, device=c.device)
+    occ = torch.empty(B, 1, H, W, dtype=torch.uint8, device=c.device)
+    rc = N.lib().dpft_ic_residual_map(ctypes.byref(c.desc), ctypes.byref(c.tens), _ptr(R), _ptr(t), _ptr(out),
+                                      _ptr(occ), _ptr(c.ws), c.ws_bytes, _stream(c.device))
+    N.check(rc, "dpft_ic_residual_map")
+    return out, occ.bool()
 
 
 def residual_level(pose, x0, x1, invD0, invD1, K, sigma0, sigma1, **kw):

@@ -8,8 +8,10 @@ on libdpft_ic.so through `TrustRegionInverseWUncertainty`; the encoder and
 init-pose networks run as PyTorch modules on the same device.
 
 Supported: track_type 'U_IC' (uncertainty_type != 'None', direction 'inverse')
-and 'IC' (uncertainty_type 'None': TrustRegionBase with M-estimator 'None' and
-solver 'Direct-Nodamping') with encoders RGB / ConvRGBD / ConvRGBD2, identity or
+and 'IC' (uncertainty_type 'None': TrustRegionBase with M-estimator 'None' or
+'MultiScale2w' and solver 'Direct-Nodamping' or 'Direct-ResVol', the weight prior
+chained across levels as LeastSquareTracking.py:346-445 does) with encoders RGB /
+ConvRGBD / ConvRGBD2, identity or
 learned init pose, remove_tru_sigma, combine_ICP, uncer_prop (returns JtWJ) and
 object masks, inference mode.  The reference's U_FC / ICP-only trackers and
 training-mode forward raise NotImplementedError -- the reference itself cannot
@@ -147,13 +149,17 @@ class LeastSquareTracking(nn.Module):
         (I0, I1, x0, x1, sigma0, sigma1, dpt0, dpt1, inv_d0, inv_d1, m0, m1, poseI) = self._preprocess(
             img0, img1, depth0, depth1, poseI=None, obj_mask0=obj_mask0, obj_mask1=obj_mask1)
         pose = poseI
-        # the weight prior of level 3 (346) only feeds learned ICP scalers / M-estimators, not offered
+        # the weight prior of level 3 (LeastSquareTracking.py:346); each level's returned
+        # weights are the next level's prior (375-445) -- read by the IC tracker's learned
+        # M-estimator, unused by the U_IC solver (its estimator call is commented out)
+        wPrior = torch.ones_like(inv_d0[3]) * 0.001
         for l in (3, 2, 1, 0):
             tr = getattr(self, f'tr_update{l}')
             Kl = K / float(1 << l)
             if self.track_type == 'IC':
-                out = tr(pose, x0[l], x1[l], inv_d0[l], inv_d1[l], Kl, None, vis_res=False,
+                out = tr(pose, x0[l], x1[l], inv_d0[l], inv_d1[l], Kl, wPrior, vis_res=False,
                          obj_mask0=m0[l], obj_mask1=m1[l])
+                wPrior = out[1]
             else:
                 out = tr(pose, x0[l], x1[l], inv_d0[l], inv_d1[l], Kl, sigma0=sigma0[l], sigma1=sigma1[l],
                          wPrior=None, vis_res=False, depth0=dpt0[l], depth1=dpt1[l], obj_mask0=m0[l],
@@ -167,9 +173,10 @@ class LeastSquareTracking(nn.Module):
         (I0, I1, x0, x1, sigma0, sigma1, dpt0, dpt1, inv_d0, inv_d1, m0, m1, poseI) = self._preprocess(
             img0, img1, depth0, depth1, poseI=poseI, obj_mask0=obj_mask0, obj_mask1=obj_mask1)
         i = level_i
-        if self.track_type == 'IC':
+        if self.track_type == 'IC':  # the IC branch's prior is all ones (LeastSquareTracking.py:641)
             loss = self.tr_update0.forward_residuals(poseI, x0[i], x1[i], inv_d0[i], inv_d1[i], K / float(1 << i),
-                                                     None, vis_res=False, obj_mask0=m0[i], obj_mask1=m1[i])
+                                                     torch.ones_like(inv_d0[i]), vis_res=False, obj_mask0=m0[i],
+                                                     obj_mask1=m1[i])
         else:
             loss = self.tr_update0.forward_residuals(
                 poseI, x0[i], x1[i], inv_d0[i], inv_d1[i], K / float(1 << i), sigma0=sigma0[i], sigma1=sigma1[i],
@@ -189,6 +196,9 @@ class LeastSquareTracking(nn.Module):
         i = level_i
         tr = self.tr_update0
         if self.track_type == 'IC':
+            if tr._learned_weights():
+                raise NotImplementedError("the multi-pose residual sweep uses unit weights; with a learned "
+                                          "M-estimator call compute_residual per pose")
             kw = dict(no_uncertainty=True, obj_mask0=m0[i], obj_mask1=m1[i])
         else:
             kw = tr._common(x0[i], dpt0[i], dpt1[i], m0[i], m1[i])

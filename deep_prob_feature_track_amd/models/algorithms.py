@@ -8,12 +8,13 @@ PyTorch fallback: configurations the kernels do not implement raise
 NotImplementedError, CPU tensors raise RuntimeError.
 
 The networks around it (feature encoder, pose initialisers, estimator
-placeholders) are PyTorch modules whose parameter names match the reference's
-state_dict keys, so the reference's checkpoints load unchanged:
+networks of the IC tracker) are PyTorch modules whose parameter names match the
+reference's state_dict keys, so the reference's checkpoints load unchanged:
   ImagePyramids 1201-1219, FeaturePyramid 1221-1430, DeepRobustEstimator
-  1432-1499, ScaleNet 1501-1581, DirectSolverNet 1583-1692 (structure; the
-  U_IC path never calls it, algorithms.py:691), PoseNetFeat / PoseNet /
-  SFMPoseNet 1694-1832, deep_damping_regressor 1834-1842.
+  1432-1499 (applied by the IC tracker), ScaleNet 1501-1581, DirectSolverNet
+  1583-1692 ('Direct-ResVol' for the IC tracker; the U_IC path never calls it,
+  algorithms.py:691), PoseNetFeat / PoseNet / SFMPoseNet 1694-1832,
+  deep_damping_regressor 1834-1842.
 """
 import torch
 import torch.nn as nn
@@ -139,7 +140,7 @@ class FeaturePyramid(nn.Module):
         return f, sigma, maps
 
 
-# ------------------------------------------------------------------ estimator placeholders
+# ------------------------------------------------------------------ estimators
 def _weight_net(D, final):
     net = nn.Sequential(conv(True, D, 16, 3, dilation=1), conv(True, 16, 32, 3, dilation=2),
                         conv(True, 32, 64, 3, dilation=4), *final)
@@ -148,9 +149,10 @@ def _weight_net(D, final):
 
 
 class DeepRobustEstimator(nn.Module):
-    """M-estimator (algorithms.py:1432-1499).  The U_IC solver never applies it
-    (the call is commented out in the reference, algorithms.py:638-641); kept for
-    the constructor / state_dict surface."""
+    """M-estimator (algorithms.py:1432-1499): 'None' (unit weights) or the
+    convolutional 'MultiScale2w' on [|r|, x0, x1, bilinear-upsampled prior weights]
+    (1467-1477; 4 input channels, so 1-channel features).  The IC tracker applies it;
+    the U_IC solver never does (commented out in the reference, 638-641)."""
 
     def __init__(self, estimator_type):
         super().__init__()
@@ -199,10 +201,37 @@ def deep_damping_regressor(D):
     return nn.Sequential(fcLayer(D, 128), fcLayer(128, 256), fcLayer(256, 6))
 
 
+def _twist2mat(w):
+    """Exp of so(3) vectors [B,3] by Rodrigues (geometry.py:163-185); NaN at |w| = 0 as there."""
+    th = torch.sqrt((w * w).sum(1, keepdim=True))
+    k = w / th
+    K = torch.zeros(w.shape[0], 3, 3, dtype=w.dtype, device=w.device)
+    K[:, 0, 1], K[:, 0, 2] = -k[:, 2], k[:, 1]
+    K[:, 1, 0], K[:, 1, 2] = k[:, 2], -k[:, 0]
+    K[:, 2, 0], K[:, 2, 1] = -k[:, 1], k[:, 0]
+    s, c = torch.sin(th).view(-1, 1, 1), torch.cos(th).view(-1, 1, 1)
+    I = torch.eye(3, dtype=w.dtype, device=w.device).expand_as(K)
+    return I + s * K + (1 - c) * torch.bmm(K, K)
+
+
+def inverse_update_pose(H, JtR, pose):
+    """xi = H^-1 JtR, R <- R Exp(-w), t <- R (-Exp(-w) v) + t (algorithms.py:2017-2054),
+    batched on the device in fp64 (the reference inverts on the host CPU in fp32, 2077-2091)."""
+    R, t = pose
+    B = H.shape[0]
+    xi = torch.linalg.solve(H.double(), JtR.double().reshape(B, 6, 1)).view(B, 6)
+    dR = _twist2mat(-xi[:, :3])
+    dt = -torch.bmm(dR, xi[:, 3:].reshape(B, 3, 1))
+    R1, t1 = geometry.batch_Rt_compose(R.double(), t.double(), dR, dt)
+    return [R1.to(R.dtype), t1.to(t.dtype).view(B, 3, 1)]
+
+
 class DirectSolverNet(nn.Module):
-    """Damping module (algorithms.py:1583-1692).  The U_IC solver does not call it
-    (it always uses lev_mar_H, algorithms.py:836-846); kept for the surface and the
-    'Direct-ResVol' parameters."""
+    """Damping module (algorithms.py:1583-1692).  The U_IC solver does not call it (it
+    always uses lev_mar_H, algorithms.py:836-846); the IC tracker (TrustRegionBase) runs
+    'Direct-Nodamping' inside the fused HIP iteration and 'Direct-ResVol' through
+    `resvol_step`: the residual volume's ten J^T W r samples come from the HIP kernel
+    (DPFT_ITER_NO_UPDATE), the damping MLP and the 6x6 solves from PyTorch."""
 
     SOLVER_NO_DAMPING = 0
     SOLVER_RESIDUAL_VOLUME = 1
@@ -222,7 +251,35 @@ class DirectSolverNet(nn.Module):
             raise NotImplementedError()
 
     def forward(self, *args, **kwargs):
-        raise NotImplementedError("DirectSolverNet is not on the U_IC path (algorithms.py:691)")
+        raise NotImplementedError("DirectSolverNet is driven by TrustRegionBase (resvol_step); not on the U_IC path")
+
+    def resvol_step(self, pose, level_args, weights, obj_mask0, obj_mask1, first):
+        """One Gauss-Newton step with the learned residual-volume damping
+        (__regularize_residual_volume, algorithms.py:1644-1691, then inverse_update_pose):
+        JtWJ, JtWr at `pose` (obj_mask0 only on a level's first step, 72-73 / 77-78), ten
+        trial poses under damping lambda_s diag(JtWJ) + 1e-6 tr(JtWJ) I with lambda_s in
+        logspace(-5, 5), the J^T W r of each trial (masks of frame 1 only, 1683), the MLP
+        on [JtR_1 .. JtR_10, JtWJ] -> per-axis damping, and the damped update."""
+        x0, x1, invD0, invD1, K = level_args
+        B = x0.shape[0]
+        R, t, JtJ, JtR, _ = ic.iterate(pose, x0, x1, invD0, invD1, K, None, None, first=first, update=False,
+                                       no_uncertainty=True, weights=weights, obj_mask0=obj_mask0,
+                                       obj_mask1=obj_mask1)
+        pose = [R, t]
+        diag_mask = torch.eye(6, dtype=JtJ.dtype, device=JtJ.device).view(1, 6, 6)
+        diagJtJ = diag_mask * JtJ
+        epsilon = (torch.sum(diagJtJ, (2, 1)) * 1e-6).view(B, 1, 1) * diag_mask
+        lambdas = torch.logspace(-5, 5, self.samples, dtype=JtJ.dtype, device=JtJ.device)
+        vols = []
+        for s in range(self.samples):
+            pose_s = inverse_update_pose(JtJ + lambdas[s] * diagJtJ + epsilon, JtR, pose)
+            _, _, _, JtR_s, _ = ic.iterate(pose_s, x0, x1, invD0, invD1, K, None, None, first=False, update=False,
+                                           no_uncertainty=True, weights=weights, obj_mask1=obj_mask1)
+            vols.append(JtR_s.view(B, 6, 1))
+        JtR_flat = torch.cat(vols, dim=2).view(B, -1)
+        damp = self.net(torch.cat((JtR_flat, JtJ.view(B, -1)), dim=1))
+        H = JtJ + diag_mask * damp.view(B, 6, 1) + epsilon
+        return inverse_update_pose(H, JtR, pose)
 
 
 # ------------------------------------------------------------------ init-pose networks
@@ -324,10 +381,14 @@ class TrustRegionBase(nn.Module):
     forward -> (pose [R, t], weights): the constant J^T W J of the template
     (precompute_Jacobian 103-121, identical in every iteration, so the fused kernel
     simply recomputes it), JtR of the residual at the current pose with occluded
-    residuals 1e-3 (compute_warped_residual 1919-1957), lev_mar_H damping and the
-    inverse update (DirectSolverNet 'Direct-Nodamping', 1604-1642).  As in the
-    reference, only the first residual sees obj_mask0 (the loop re-evaluates with
-    obj_mask1 alone, 77-78).  Supported: mEstimator 'None', solver 'Direct-Nodamping'."""
+    residuals 1e-3 (compute_warped_residual 1919-1957), and the damped inverse update.
+    M-estimator (66-68): 'None' = unit weights; 'MultiScale2w' = the convolutional
+    estimator on [|r|, x0, x1, upsampled wPrior] of the first residual (the HIP
+    residual map, dpft_ic_residual_map), whose per-pixel weights the fused kernel then
+    applies to J^T W J and J^T W r in every iteration.  Solver: 'Direct-Nodamping'
+    (lev_mar_H, solved in-kernel) or 'Direct-ResVol' (DirectSolverNet.resvol_step).  As
+    in the reference, only the first residual sees obj_mask0 (the loop re-evaluates with
+    obj_mask1 alone, 77-78)."""
 
     def __init__(self, max_iter=3, mEst_func=None, solver_func=None, timers=None):
         super().__init__()
@@ -339,29 +400,51 @@ class TrustRegionBase(nn.Module):
     def _check(self, x0):
         if torch.is_grad_enabled() and x0.requires_grad:
             raise NotImplementedError("the HIP IC solver is inference-only (no backward kernels)")
-        if self.mEstimator is not None and getattr(self.mEstimator, 'D', -1) > 0:
-            raise NotImplementedError("learned M-estimators are not supported by the fused HIP solver")
-        if self.directSolver is not None and getattr(self.directSolver, 'type', 0) != DirectSolverNet.SOLVER_NO_DAMPING:
-            raise NotImplementedError("only the 'Direct-Nodamping' solver is supported by the fused HIP solver")
+
+    def _learned_weights(self):
+        return self.mEstimator is not None and getattr(self.mEstimator, 'D', -1) > 0
+
+    def _weights(self, pose, x0, x1, invD0, invD1, K, wPrior, obj_mask0, obj_mask1):
+        """(weights [B,1,H,W] of the learned estimator, residual map, occlusion) or Nones."""
+        if not self._learned_weights():
+            return None, None, None
+        if wPrior is None:
+            raise ValueError("a learned M-estimator needs the weight prior wPrior (LeastSquareTracking.py:346)")
+        res, occ = ic.residual_map(pose, x0, x1, invD0, invD1, K, obj_mask0=obj_mask0, obj_mask1=obj_mask1)
+        return self.mEstimator(res, x0, x1, wPrior), res, occ
 
     def forward(self, pose, x0, x1, invD0, invD1, K, wPrior=None, vis_res=False, obj_mask0=None, obj_mask1=None):
         self._check(x0)
         B, C, H, W = x0.shape
+        resvol = getattr(self.directSolver, 'type', 0) == DirectSolverNet.SOLVER_RESIDUAL_VOLUME
         with torch.no_grad():
+            w, _, _ = self._weights(pose, x0, x1, invD0, invD1, K, wPrior, obj_mask0, obj_mask1)
             for it in range(self.max_iterations):
-                R, t, _, _, _ = ic.iterate(pose, x0, x1, invD0, invD1, K, None, None, first=(it == 0),
-                                           no_uncertainty=True, obj_mask0=obj_mask0 if it == 0 else None,
-                                           obj_mask1=obj_mask1)
-                pose = [R, t]
-        weights = torch.ones((1, 1, 1, 1), dtype=x0.dtype, device=x0.device).expand(B, C, H, W)
+                m0 = obj_mask0 if it == 0 else None
+                if resvol:
+                    pose = self.directSolver.resvol_step(pose, (x0, x1, invD0, invD1, K), w, m0, obj_mask1,
+                                                         first=(it == 0))
+                else:
+                    R, t, _, _, _ = ic.iterate(pose, x0, x1, invD0, invD1, K, None, None, first=(it == 0),
+                                               no_uncertainty=True, weights=w, obj_mask0=m0, obj_mask1=obj_mask1)
+                    pose = [R, t]
+        weights = w if w is not None else torch.ones((1, 1, 1, 1), dtype=x0.dtype, device=x0.device).expand(B, C, H, W)
         return pose, weights
 
     def forward_residuals(self, pose, x0, x1, invD0, invD1, K, wPrior=None, vis_res=False, obj_mask0=None,
                           obj_mask1=None):
+        """loss [B] (algorithms.py:125-139): the unit-weight loss in one HIP launch, or
+        with a learned estimator compute_avg_loss([weights * r], occ) (2119-2137) on the
+        HIP residual map."""
         self._check(x0)
         with torch.no_grad():
-            return ic.residual_level(pose, x0, x1, invD0, invD1, K, None, None, no_uncertainty=True,
-                                     obj_mask0=obj_mask0, obj_mask1=obj_mask1)
+            if not self._learned_weights():
+                return ic.residual_level(pose, x0, x1, invD0, invD1, K, None, None, no_uncertainty=True,
+                                         obj_mask0=obj_mask0, obj_mask1=obj_mask1)
+            w, res, occ = self._weights(pose, x0, x1, invD0, invD1, K, wPrior, obj_mask0, obj_mask1)
+            H, W = res.shape[-2:]
+            wr = torch.where(occ, torch.zeros_like(res), w * res)
+            return (wr ** 2).sum(dim=(1, 2, 3)) / (H * W - occ.sum(dim=(1, 2, 3)))
 
 
 class TrustRegionInverseWUncertainty(nn.Module):

@@ -21,6 +21,7 @@
  *   dpft_ic_solve_pyramid  <- the coarse-to-fine level loop of LeastSquareTracking.forward
  *                             code/models/LeastSquareTracking.py:349-445 (tr_update3..0)
  *   dpft_ic_iterate        <- ONE pass of the loop body algorithms.py:646-693
+ *   dpft_ic_residual_map   <- compute_warped_residual algorithms.py:1919-1957 (IC tracker)
  *   dpft_ic_residual_level <- TrustRegionInverseWUncertainty.forward_residuals
  *                             algorithms.py:725-786 (+ compute_avg_loss 2119-2137)
  *   dpft_workspace_size / dpft_version / dpft_last_error: library plumbing.
@@ -51,7 +52,7 @@
 extern "C" {
 #endif
 
-#define DPFT_ABI_VERSION 1
+#define DPFT_ABI_VERSION 2
 
 /* flags of DpftLevelDesc */
 #define DPFT_REMOVE_TRU_SIGMA 0x1u /* --remove_tru_sigma (algorithms.py:1975-1980) */
@@ -117,6 +118,9 @@ typedef struct DpftLevelTensors {
     const uint8_t* mask1; /* [B,1,H,W]  object mask of frame 1, nullable        */
     const float* K;       /* [B,4]      (fx,fy,cx,cy) of THIS level             */
     uint32_t* status;     /* [1]        device status word, OR-ed, never cleared */
+    const float* weights; /* [B,1,H,W]  per-pixel M-estimator weights, nullable;
+                             DPFT_NO_UNCERTAINTY only (TrustRegionBase with a learned
+                             DeepRobustEstimator, algorithms.py:71-76, 1631-1632)  */
 } DpftLevelTensors;
 
 /* Bytes of workspace the level needs (>= 256-byte aligned pointer expected).
@@ -150,7 +154,9 @@ int dpft_ic_solve_pyramid(const DpftLevelDesc* descs, const DpftLevelTensors* te
 /*
  * One iteration (residual -> Jacobian -> JtJ/JtR -> damped solve -> update).
  * `first`: bit 0 (DPFT_ITER_FIRST) must be set on the first iteration of a level
- * (it computes the per-level sigma0 extrema); bit 1 (DPFT_ITER_REVERSE) walks the
+ * (it computes the per-level sigma0 extrema); bit 2 (DPFT_ITER_NO_UPDATE) only writes
+ * jtj_out / jtr_out (the damped solve and the pose update are skipped); bit 1
+ * (DPFT_ITER_REVERSE) walks the
  * level in the reverse order (dpft_ic_solve_level sets it on odd iterations, so
  * an iteration starts on the bytes the previous one read last, still in the
  * Infinity Cache; same arithmetic, different fp32 summation grouping).
@@ -159,6 +165,9 @@ int dpft_ic_solve_pyramid(const DpftLevelDesc* descs, const DpftLevelTensors* te
  */
 #define DPFT_ITER_FIRST 1u
 #define DPFT_ITER_REVERSE 2u
+#define DPFT_ITER_NO_UPDATE 4u /* normal equations only (jtj_out / jtr_out), R / t untouched:
+                                  the residual-volume samples of DirectSolverNet 'Direct-ResVol'
+                                  (algorithms.py:1668-1685)                                    */
 int dpft_ic_iterate(const DpftLevelDesc* desc, const DpftLevelTensors* tensors,
                     float* R, float* t, float* jtj_out, float* jtr_out, int32_t* invalid_out,
                     int first, void* workspace, size_t workspace_bytes, void* hip_stream);
@@ -193,6 +202,17 @@ int dpft_ic_residual_poses(const DpftLevelDesc* desc, const DpftLevelTensors* te
  */
 int dpft_sigma_extrema_levels(const DpftLevelDesc* descs, const DpftLevelTensors* tensors, int32_t levels,
                               void* workspace, size_t workspace_bytes, void* hip_stream);
+
+/*
+ * The IC tracker's residual map at pose (R, t) (compute_warped_residual,
+ * algorithms.py:1919-1957; DPFT_NO_UNCERTAINTY): out [B,C,H,W] fp32 NCHW =
+ * bilinear(f1, warp) - f0 with 1e-3 on occluded / masked pixels, occ_out [B,1,H,W]
+ * uint8 (nullable) = those pixels.  The input of the learned M-estimator
+ * (DeepRobustEstimator 'MultiScale2w', algorithms.py:1467-1477) and of its weighted
+ * residual loss (forward_residuals 125-139).
+ */
+int dpft_ic_residual_map(const DpftLevelDesc* desc, const DpftLevelTensors* tensors, const float* R, const float* t,
+                         float* out, uint8_t* occ_out, void* workspace, size_t workspace_bytes, void* hip_stream);
 
 /* Kernel-only timing hook for the roofline: launch ONLY the fused residual +
  * Jacobian + normal-equation kernel (no finalize), using the sigma0 extrema a

@@ -140,6 +140,40 @@ def normal_equations(J, rw):
     return torch.bmm(Jf.transpose(1, 2), Jf), torch.bmm(Jf.transpose(1, 2), rw.reshape(B, -1, 1))
 
 
+# --------------------------------------------------------------------------- IC tracker (no uncertainty)
+def ic_residuals(R, t, invD0, invD1, f0, f1, x, y, K, mask0=None, mask1=None):
+    """compute_warped_residual, algorithms.py:1919-1957: r = f1(warp) - f0, 1e-3 where
+    occluded / masked.  Returns (r [B,C,H,W], occ [B,1,H,W])."""
+    B, C, H, W = f0.shape
+    u, v, iz = warp_inverse_depth(x, y, invD0, R, t, K)
+    occ = occlusion(iz, invD1, u, v)
+    if mask0 is not None:
+        occ = occ | ~mask0.view(B, 1, H, W)
+    if mask1 is not None:
+        occ = occ | ~(bilinear(mask1.to(f0.dtype), u, v) > 0).view(B, 1, H, W)
+    r = bilinear(f1, u, v) - f0
+    return torch.where(occ.expand(B, C, H, W), torch.full_like(r, 1e-3), r), occ
+
+
+def ic_jacobian(invD0, f0, x, y, K):
+    """precompute_Jacobian, algorithms.py:103-121: J = gx Jx + gy Jy per channel
+    (compute_jacobian_dIdp 1867-1882) -> [B, C*HW, 6]."""
+    B, C, H, W = f0.shape
+    gx, gy = sobel(f0)
+    Jx, Jy = warp_jacobian(invD0, K, x, y)
+    J = gx.view(B, C, -1, 1) * Jx.view(B, 1, -1, 6) + gy.view(B, C, -1, 1) * Jy.view(B, 1, -1, 6)
+    return J.view(B, -1, 6)
+
+
+def ic_normal_equations(J, r, weights=None):
+    """JtWJ = J^T (w J) (algorithms.py:71-76), JtR = J^T (w r) (DirectSolverNet 1631-1632);
+    weights [B,1,H,W] (one per pixel, C = 1) or None (unit)."""
+    B = J.shape[0]
+    w = torch.ones_like(r) if weights is None else weights.expand_as(r)
+    wJ = w.reshape(B, -1, 1) * J
+    return torch.bmm(J.transpose(1, 2), wJ), torch.bmm(J.transpose(1, 2), (w * r).reshape(B, -1, 1))
+
+
 # --------------------------------------------------------------------------- ICP term
 def vertex_map(depth, x, y):
     """[x,y,1] * depth.  geometry.py:1129-1136."""

@@ -278,3 +278,48 @@ def test_preprocess_depth_bit_exact(B, H, W, levels, extreme):
         wantd = F.max_pool2d(depth, k, k) if k > 1 else depth
         assert torch.equal(inv[l].cpu(), want), f"invD level {l}"
         assert torch.equal(dep[l].cpu(), wantd), f"depth level {l}"
+
+
+@pytest.mark.parametrize("B,C,H,W,masks,packed", [(2, 1, 37, 70, True, False), (1, 8, 60, 80, False, True),
+                                                  (3, 3, 17, 129, True, False)])
+def test_ic_residual_map_and_weighted_normal_equations(B, C, H, W, masks, packed):
+    """The IC tracker's residual map (dpft_ic_residual_map) and, with per-pixel M-estimator
+    weights, its normal equations (dpft_ic_iterate with DPFT_ITER_NO_UPDATE) against the
+    CPU oracle's compute_warped_residual / J^T W J / J^T W r (algorithms.py:71-76,
+    103-121, 1631-1632, 1919-1957); then one weighted update equals the oracle's damped
+    solve of the same normal equations."""
+    from deep_prob_feature_track_amd import ic
+    from oracle import ic_oracle as O
+    dev = _dev()
+    f0, f1, _, _, invD0, invD1, K, m0, m1 = _random_case(B, C, 1, H, W, seed=7 * B + C + W, masks=masks)
+    g = torch.Generator().manual_seed(3 + C)
+    w = torch.rand(B, 1, H, W, generator=g)
+    R = torch.eye(3).repeat(B, 1, 1)
+    R[:, 0, 1], R[:, 1, 0] = 0.01, -0.01
+    t = torch.full((B, 3, 1), 0.002)
+    x, y = O.pixel_rays(B, H, W, K)
+    r_o, occ_o = O.ic_residuals(R, t, invD0, invD1, f0, f1, x, y, K, mask0=m0, mask1=m1)
+    J = O.ic_jacobian(invD0, f0, x, y, K)
+    cu = lambda a: a.to(dev) if a is not None else None
+    x0, x1 = (ic.pack_features(cu(f0)), ic.pack_features(cu(f1))) if packed else (cu(f0), cu(f1))
+    r_g, occ_g = ic.residual_map((cu(R), cu(t)), x0, x1, cu(invD0), cu(invD1), cu(K), obj_mask0=cu(m0),
+                                 obj_mask1=cu(m1))
+    assert torch.equal(occ_g.cpu(), occ_o)
+    # a few ulps: the CPU grid sampler's multi-channel path does not always round as the
+    # single-channel fma chain the kernel reproduces (2 of 38400 values at C = 8)
+    torch.testing.assert_close(r_g.cpu(), r_o, rtol=0, atol=1e-5)
+    for weights in (None, w):
+        JtJ_o, JtR_o = O.ic_normal_equations(J.double(), r_o.double(), None if weights is None else weights.double())
+        Rg, tg, jtj, jtr, inv = ic.iterate((cu(R), cu(t)), x0, x1, cu(invD0), cu(invD1), cu(K), None, None,
+                                           update=False, no_uncertainty=True, weights=cu(weights),
+                                           obj_mask0=cu(m0), obj_mask1=cu(m1))
+        assert torch.equal(Rg.cpu(), R) and torch.equal(tg.cpu(), t)  # NO_UPDATE leaves the pose
+        assert int(inv.sum()) == int(occ_o.sum())
+        rel = (jtj.cpu().double() - JtJ_o).abs().max() / JtJ_o.abs().max()
+        relr = (jtr.cpu().double() - JtR_o.view(B, 6)).abs().max() / JtR_o.abs().max()
+        assert rel < 1e-5 and relr < 1e-4, f"weights={weights is not None}: JtJ rel {rel:.2e}, JtR rel {relr:.2e}"
+    # the weighted update: the kernel's damped solve of its own normal equations
+    R1, t1, jtj, jtr, _ = ic.iterate((cu(R), cu(t)), x0, x1, cu(invD0), cu(invD1), cu(K), None, None,
+                                     no_uncertainty=True, weights=cu(w), obj_mask0=cu(m0), obj_mask1=cu(m1))
+    Ro, to, _ = O.damped_solve_update(jtj.cpu().double(), jtr.cpu().double().view(B, 6, 1), R.double(), t.double())
+    assert (R1.cpu().double() - Ro).abs().max() < 1e-5 and (t1.cpu().double().view(B, 3) - to.view(B, 3)).abs().max() < 1e-5

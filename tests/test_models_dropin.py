@@ -21,8 +21,9 @@ HERE = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
 KEYS = json.load(open(os.path.join(HERE, "model_keys.json")))
 
 
-def build(spec, mest="None", solver="Direct-Nodamping", no_weight_sharing=False):
-    return LeastSquareTracking(spec["encoder"], spec["uncertainty"], 3, mest, solver,
+def build(spec, mest=None, solver=None, no_weight_sharing=False):
+    return LeastSquareTracking(spec["encoder"], spec["uncertainty"], 3, mest or spec.get("mest", "None"),
+                               solver or spec.get("solver", "Direct-Nodamping"),
                                options=default_options(**spec["opts"]), no_weight_sharing=no_weight_sharing)
 
 
