@@ -4,7 +4,12 @@
 One *step* = one full coarse-to-fine solve (levels 3..0, 3 Gauss-Newton
 iterations each = 12 IC iterations per pair) of a batch of B frame pairs per
 GPU, replayed from one HIP graph, followed (N > 1) by the RCCL all-gather of
-the per-pair poses.  Workload: cfg3's shard -- B = 8 pairs per GPU cycled from
+the per-pair poses.  An eval stream keeps --inflight batches (default 3, distinct
+pairs each) in flight per GPU: step k replays slot k % inflight's graph on that
+slot's stream, so one batch's latency-bound coarse levels overlap another's
+bandwidth-bound level 0; every batch is solved exactly as alone (batch-global
+masks over its own B pairs, bit-identical poses).  `latency_ms_per_solve` is one
+solve with nothing else in flight.  Workload: cfg3's shard -- B = 8 pairs per GPU cycled from
 the ordered pairs of the five TUM fr1/desk frames, deterministic features
 (tests/golden/recipe.py), inputs resident in HBM before the timed region.
 
@@ -35,6 +40,9 @@ def parse():
     p.add_argument("--steps", type=int, default=100)
     p.add_argument("--warmup", type=int, default=10)
     p.add_argument("--batch-per-gpu", type=int, default=8)
+    p.add_argument("--inflight", type=int, default=3,
+                   help="independent B-pair batches in flight per GPU (one stream, graph, workspace and input "
+                        "set each; each batch's solve is unchanged, bit for bit)")
     p.add_argument("--kernel-reps", type=int, default=50)
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--no-graph", action="store_true")
@@ -177,7 +185,11 @@ def main():
     from deep_prob_feature_track_amd import ic, shard
 
     B = a.batch_per_gpu
-    sel, levels_nchw, K = make_inputs(B, rank, device)
+    S = max(1, a.inflight)
+    # batch j of this rank: the pairs of make_inputs "rank" rank * S + j (distinct pairs per
+    # in-flight slot and rank, cycled through the 20 ordered pairs of the 5 frames)
+    slot_inputs = [make_inputs(B, rank * S + j, device) for j in range(S)]
+    sel, levels_nchw, K = slot_inputs[0]
 
     def packed(levels):
         return [dict(d, x0=ic.pack_features(d["x0"]), x1=ic.pack_features(d["x1"])) for d in levels]
@@ -197,7 +209,7 @@ def main():
     # R [B,3,3] and t [B,3] as two contiguous views of one buffer: one reset copy per step
     pose_init = torch.cat((torch.eye(3, device=device).repeat(B, 1, 1).reshape(-1), torch.zeros(B * 3, device=device)))
 
-    def make_step(levels):
+    def make_step(levels, K=K):
         solver = ic.PyramidSolver(levels, K, iters=ITERS, remove_tru_sigma=True,
                                   schedule=os.environ.get("DPFT_BENCH_SCHEDULE"))  # A/B only
         pose = pose_init.clone()
@@ -230,10 +242,18 @@ def main():
                 solve()
         return solver, R, t, run, graph is not None
 
-    solver, R, t, run, graphed = make_step(levels)
+    # S in-flight slots: slot j solves its own batch on its own stream from its own HIP
+    # graph and workspace; step k runs on slot k % S, so a batch's latency-bound coarse
+    # levels and finalizes overlap another batch's bandwidth-bound level 0
+    slots = []
+    for j in range(S):
+        lv = levels if j == 0 else (packed(slot_inputs[j][1]) if a.layout == "c4" else slot_inputs[j][1])
+        slots.append(make_step(lv, slot_inputs[j][2]))
+    streams = [torch.cuda.Stream(device) for _ in range(S)]
+    solver, R, t, run, graphed = slots[0]
     # N > 1: the pose gather of step k runs on the collective stream while step k + 1
-    # solves (double-buffered output; poses packed into a fresh buffer first); every
-    # gather is waited for inside the timed region (drain())
+    # solves (double-buffered output; poses packed into a fresh buffer first, on the
+    # slot's stream); every gather is waited for inside the timed region (drain())
     gathered = [torch.empty(world * B, 12, device=device) for _ in range(2)] if world > 1 else None
     pending = [None]
     nstep = [0]
@@ -244,11 +264,14 @@ def main():
             pending[0] = None
 
     def step():
-        run()
-        if world > 1:
-            drain()
-            _, pending[0] = shard.gather_poses(R, t, out=gathered[nstep[0] % 2], async_op=True)
-            nstep[0] += 1
+        j = nstep[0] % S
+        with torch.cuda.stream(streams[j]):
+            slots[j][3]()
+            if world > 1:
+                drain()
+                _, pending[0] = shard.gather_poses(slots[j][1], slots[j][2], out=gathered[nstep[0] % 2],
+                                                   async_op=True)
+        nstep[0] += 1
 
     def barrier():
         if world > 1:
@@ -274,10 +297,21 @@ def main():
         e = torch.tensor([elapsed], device=device, dtype=torch.float64)
         dist.all_reduce(e, op=dist.ReduceOp.MAX)
         elapsed = e.item()
-    ic.check_status(solver.status)
+    for sl in slots:
+        ic.check_status(sl[0].status)
     ms_per_step = elapsed / a.steps * 1e3
     iters_total = world * B * LEVELS * ITERS * a.steps
     value = iters_total / elapsed
+    # latency of one solve (slot 0 alone, back to back on one stream), rank 0 only
+    latency_ms = None
+    if rank == 0:
+        n_lat = min(a.steps, 50)
+        torch.cuda.synchronize()
+        tl0 = time.perf_counter()
+        for _ in range(n_lat):
+            run()
+        torch.cuda.synchronize()
+        latency_ms = (time.perf_counter() - tl0) / n_lat * 1e3
 
     # ---- roofline of the dominant kernel: the level-0 fused reduce (+ its in-kernel
     # finalize), i.e. exactly the launches the solve makes at level 0 -- iterations
@@ -344,7 +378,8 @@ def main():
             "config": {"workload": "cfg2/cfg3 shard: 640x480, C=32, Cs=1, 4 levels x 3 GN iters, "
                                    "remove_tru_sigma, B pairs per GPU", "pairs_per_gpu": B,
                        "global_batch": world * B, "parallelism": f"pair-sharded x{world}, RCCL all-gather of poses",
-                       "graph": graphed, "feature_layout": a.layout},
+                       "graph": graphed, "feature_layout": a.layout, "inflight": S},
+            "latency_ms_per_solve": latency_ms,
             "pairs_per_s": world * B * a.steps / elapsed,
             "l0_iters_per_s": world * B * ITERS * a.steps / elapsed,
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
