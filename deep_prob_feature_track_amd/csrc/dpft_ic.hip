@@ -125,6 +125,12 @@ constexpr bool kMarchReverse = DPFT_MARCH_REVERSE != 0;  // honour DPFT_ITER_REV
 #define DPFT_MARCH_SKEW 10
 #endif
 constexpr int kMarchSkew = DPFT_MARCH_SKEW;  // band-size skew of the marching schedule (64ths, 0..63)
+#ifndef DPFT_MARCH_GRID
+#define DPFT_MARCH_GRID 1
+#endif
+// marching bands on a (row band x strip) grid: every strip cut at the same rows, so the
+// waves of horizontally adjacent strips read their shared columns at the same time
+constexpr bool kMarchGrid = DPFT_MARCH_GRID != 0;
 constexpr int kMarchRows = DPFT_MARCH_ROWS;  // rows per marching step (1, or 2: -10 % f1 traffic, +11 % VALU, 4 % slower)
 constexpr int kRingM = DPFT_RING_M;       // quads in flight on the marching path (kRingM - 1 ahead)
 #ifndef DPFT_UNROLL_Q
@@ -1408,17 +1414,36 @@ __global__ __launch_bounds__(kThreads, DPFT_MIN_WAVES) void ic_reduce_kernel(Ite
     // first, which the oldest-first issue arbitration favours over the second
     // workgroup on the same CU; equal bands leave the second half running alone
     // (at half occupancy) for ~20 % of the launch.  Weights 64 + skew / 64 - skew.
-    auto band_start = [&](int bnd) {
-      const int h = nw >> 1, sk = nw >= 2 ? p.skew : 0;
+    // n bands of a total of `len` units, weights 64 + skew for the first half, 64 - skew
+    auto split_start = [&](int bnd, int n, int len) {
+      const int h = n >> 1, sk = n >= 2 ? p.skew : 0;
       const long wsum = (long)(64 + sk) * min(bnd, h) + (long)(64 - sk) * max(bnd - h, 0);
-      const long wtot = (long)(64 + sk) * h + (long)(64 - sk) * (nw - h);
-      return (int)(((long)U * wsum) / wtot);
+      const long wtot = (long)(64 + sk) * h + (long)(64 - sk) * (n - h);
+      return (int)(((long)len * wsum) / wtot);
     };
-    const int ubeg = band_start(band), uend = band_start(band + 1);
+    // Grid split (kMarchGrid): K row bands x S strips, band = k * S + s, every strip cut
+    // at the same rows.  A strip's 64 lanes read columns 62 s - 1 .. 62 s + 62, so the
+    // 128-byte lines at a strip boundary belong to both strips (1.15x f0 lines per row);
+    // with a common row cut the two waves read them within a row-step of each other (an
+    // L2 hit for the second) instead of tens of microseconds apart.  Up to nw / 16 waves
+    // may be left without a band (nw - K S); otherwise the strip-major split below.
+    const int S_ = p.tiles_x, K_ = nw / S_;
+    const bool grid = kMarchGrid && K_ >= 2 && (nw - K_ * S_) * 16 <= nw;
+    int ubeg, uend, vband;
+    if (grid) {
+      const int k = band / S_, s = band - k * S_;
+      ubeg = k < K_ ? s * H + split_start(k, K_, H) : 0;
+      uend = k < K_ ? s * H + split_start(k + 1, K_, H) : 0;
+      vband = k;
+    } else {
+      ubeg = split_start(band, nw, U);
+      uend = split_start(band + 1, nw, U);
+      vband = band;
+    }
     const int nrows = uend - ubeg;
     // odd iterations reverse every band: they start on the rows the previous iteration
     // read last, which are still in the Infinity Cache
-    const bool up = ((band & 1) != 0) != (kMarchReverse && p.reverse != 0);
+    const bool up = ((vband & 1) != 0) != (kMarchReverse && p.reverse != 0);
     const int dir = up ? -1 : 1;
     const float dirf = up ? -1.0f : 1.0f;
     const int row_restart = up ? H - 1 : 0;  // a strip begins here in marching order
@@ -1445,6 +1470,7 @@ __global__ __launch_bounds__(kThreads, DPFT_MIN_WAVES) void ic_reduce_kernel(Ite
     // otherwise misses the XCD's L2 one row-step later.
     f32x4 tc[kTapCache ? NQW : 1][2];
     int tc_ob = -1;
+
     // d of the next step's (up to) two rows, prefetched one step ahead
     float dnx[2] = {0.f, 0.f};
     auto load_d2 = [&](int k, float (&dd)[2]) {
@@ -1613,9 +1639,17 @@ __global__ __launch_bounds__(kThreads, DPFT_MIN_WAVES) void ic_reduce_kernel(Ite
           // D in marching order: gy carries the sign dirf, folded into the odd sums
           // (gx gy, gy res, gy) once per row below
           const f32x2 D = fn - fp;
-          const f32x2 x = f32x2{lane_from_right(V.x) - lane_from_left(V.x), lane_from_right(V.y) - lane_from_left(V.y)};
-          const f32x2 yv =
-              f32x2{lane_from_left(D.x) + lane_from_right(D.x), lane_from_left(D.y) + lane_from_right(D.y)} + 2.0f * D;
+          // scalar lane differences: one of each pair of lane shifts folds into the
+          // v_sub / v_add as its DPP operand (a packed v_pk_add cannot take one)
+          const float xl0 = lane_from_left(V.x), xl1 = lane_from_left(V.y);
+          const float dl0 = lane_from_left(D.x), dl1 = lane_from_left(D.y);
+          float x0 = lane_from_right(V.x) - xl0, x1 = lane_from_right(V.y) - xl1;
+          float y0 = lane_from_right(D.x) + dl0, y1 = lane_from_right(D.y) + dl1;
+          // opaque to the SLP vectorizer, which would pack each pair into one v_pk_add
+          // and keep both shifts as v_mov_dpp
+          asm("" : "+v"(x0), "+v"(x1), "+v"(y0), "+v"(y1));
+          const f32x2 x = f32x2{x0, x1};
+          const f32x2 yv = f32x2{y0, y1} + 2.0f * D;
           const f32x2 n2 = x * x + (yv * yv + 1e-8f);
           const f32x2 inv = f32x2{__builtin_amdgcn_rsqf(n2.x), __builtin_amdgcn_rsqf(n2.y)};
           const f32x2 gx = x * inv, gy = yv * inv;

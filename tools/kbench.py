@@ -8,7 +8,7 @@ sys.path[:0] = [ROOT, os.path.join(ROOT, "tests", "golden")]
 import torch
 if os.environ.get("DPFT_LIB"):
     from deep_prob_feature_track_amd import _native as _N0
-    _N0.LIB_PATH = os.environ["DPFT_LIB"]
+    _N0.LIB_PATH = os.path.abspath(os.environ["DPFT_LIB"])
 import bench
 from deep_prob_feature_track_amd import ic
 
@@ -21,6 +21,7 @@ p.add_argument("--mode", choices=["reduce", "iterate", "level"], default="reduce
 p.add_argument("--c4", action="store_true", help="channel-quad packed features")
 p.add_argument("--schedule", default=None, help="auto | march | split (channel-quad reduce kernel)")
 p.add_argument("--tail", action="store_true", help="print the launch timeline of a DPFT_TAIL_PROF build")
+p.add_argument("--warm-ms", type=float, default=300.0, help="warm-up time before timing")
 p.add_argument("--from-solve", action="store_true",
                help="start from the poses of one full pyramid solve (the bench's operating point) instead of identity")
 a = p.parse_args()
@@ -50,8 +51,15 @@ for level in ([a.level] if a.level >= 0 else range(len(solver.calls))):
     run = {"reduce": lambda: solver.reduce_only(level, R, t), "iterate": lambda: solver.iterate(level, R, t),
            "level": run_level}[a.mode]
     per = 3 if a.mode == "level" else 1
-    for _ in range(3):
-        run()
+    # warm-up by wall time: the GPU clocks ramp over the first tens of milliseconds of load
+    # (a 60-launch loop right after start-up times ~20 % slow)
+    import time
+    torch.cuda.synchronize()
+    tw = time.perf_counter()
+    while time.perf_counter() - tw < a.warm_ms * 1e-3:
+        for _ in range(3):
+            run()
+        torch.cuda.synchronize()
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     e0.record()
     for _ in range(a.reps):

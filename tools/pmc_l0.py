@@ -3,7 +3,8 @@
 
     python tools/pmc_l0.py --out profiles/r1_l0_traffic.json
 
-Runs tools/kbench.py (level 0, channel-quad, `iterate` = the launch bench.py times)
+Runs tools/kbench.py (level 0, channel-quad, `level --from-solve` = the forward / reverse /
+forward launch group bench.py times, from the solved poses)
 under two separate `rocprofv3 --pmc` passes (FETCH_SIZE; WRITE_SIZE) and writes the
 per-launch bytes, corrected as MI355X_MICROARCH.md's HBM section prescribes:
 FETCH_SIZE counts half the bytes of a 128-B-request stream on gfx950 (TCC_EA0_RDREQ
@@ -24,6 +25,9 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 SRC = os.path.join(ROOT, "deep_prob_feature_track_amd", "csrc", "dpft_ic.hip")
 
 
+SOLVE_LAUNCHES = 6
+
+
 def src_sha():
     return hashlib.sha256(open(SRC, "rb").read()).hexdigest()
 
@@ -31,13 +35,19 @@ def src_sha():
 def run_pass(counter, outdir):
     cmd = ["timeout", "-s", "KILL", "90", "rocprofv3", "--pmc", counter, "--output-format", "csv", "-d", outdir,
            "-o", "c", "--", sys.executable, os.path.join(ROOT, "tools", "kbench.py"), "--c4", "--level", "0",
-           "--mode", "iterate", "--reps", "10"]
-    subprocess.run(cmd, check=True, cwd="/tmp", env=dict(os.environ, TMPDIR="/tmp"))
-    vals = []
+           "--mode", "level", "--from-solve", "--reps", "10", "--warm-ms", "0"]
+    env = dict(os.environ, TMPDIR="/tmp")
+    if env.get("DPFT_LIB"):  # a variant library (tools/build_variants.py); the profiler runs from /tmp
+        env["DPFT_LIB"] = os.path.abspath(env["DPFT_LIB"])
+    subprocess.run(cmd, check=True, cwd="/tmp", env=env)
+    rows = []
     for f in glob.glob(os.path.join(outdir, "**", "*counter_collection.csv"), recursive=True):
         for r in csv.DictReader(open(f)):
             if "ic_reduce_kernel" in r["Kernel_Name"] and r["Counter_Name"] == counter:
-                vals.append(float(r["Counter_Value"]))
+                rows.append((int(r["Dispatch_Id"]), float(r["Counter_Value"])))
+    # the first SOLVE_LAUNCHES marching launches belong to kbench's --from-solve pyramid
+    # solve (levels 1 and 0, three each): not the timed level-0 group
+    vals = [v for _, v in sorted(rows)[SOLVE_LAUNCHES:]]
     if not vals:
         raise SystemExit(f"no ic_reduce_kernel rows for {counter}")
     return sum(vals) / len(vals), len(vals)
@@ -50,7 +60,7 @@ def main():
     tmp = os.path.join(ROOT, "gpurun_out", "pmc_l0")
     fetch, nf = run_pass("FETCH_SIZE", os.path.join(tmp, "fetch"))
     write, nw = run_pass("WRITE_SIZE", os.path.join(tmp, "write"))
-    out = {"kernel": "ic_reduce_kernel<32,Cs=1,tru,U_IC,c4> level 0, B=8, 640x480 (tools/kbench.py --mode iterate)",
+    out = {"kernel": "ic_reduce_kernel<32,Cs=1,tru,U_IC,c4> level 0, B=8, 640x480 (tools/kbench.py --mode level --from-solve)",
            "src_sha256": src_sha(), "launches": {"fetch": nf, "write": nw},
            "FETCH_SIZE_KiB": fetch, "WRITE_SIZE_KiB": write,
            "read_bytes": 2 * 1024 * fetch, "write_bytes": 1024 * write,

@@ -34,41 +34,54 @@ def main():
     mm_grids = sorted({int(r["Grid_Size_X"]) for r in rows if "minmax" in r["Kernel_Name"]})
     top = 3  # coarsest level of the 4-level bench pyramid
     ITERS = 3
-    n_red = None
+    # bench.py --inflight S replays S graphs on S side streams in the timed region; the
+    # default stream (the lowest Stream_Id) carries the solo launches: eager warm-ups, the
+    # latency loop (graph replays, nothing else in flight) and the roofline's level-0 group.
+    # Level bookkeeping is per stream.
+    streams = sorted({int(r.get("Stream_Id", 0) or 0) for r in rows})
+    solo_stream = streams[0]
+    state = collections.defaultdict(lambda: {"level": None, "n_red": None, "cur": [], "solves": []})
     groups = collections.defaultdict(list)
-    level = None
-    timeline, cur, solves = [], [], []
     for r in rows:
+        sid = int(r.get("Stream_Id", 0) or 0)
+        st = state[sid]
         name = short(r["Kernel_Name"])
         dur = (int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e3
         if name.startswith("minmax_levels"):
             # one sigma0 pre-pass for all levels opens a solve; levels then advance every
             # ITERS reduce launches (extra level-0 launches after the solve stay level 0)
-            level, n_red = top, 0
-            if cur:
-                solves.append(cur)
-                cur = []
+            st["level"], st["n_red"] = top, 0
+            if st["cur"]:
+                st["solves"].append(st["cur"])
+                st["cur"] = []
         elif "minmax" in name:
             # per-level sigma0 pass (older traces / solves without the pre-pass): the
             # smallest opens level 3, each later one the next finer level
             if int(r["Grid_Size_X"]) == mm_grids[0]:
-                level = top
+                st["level"] = top
             else:
-                level = max((level if level is not None else top) - 1, 0)
-            n_red = None
-            if level == top and cur:
-                solves.append(cur)
-                cur = []
-        elif n_red is not None and level is not None and name.startswith(("ic_reduce", "ic_split")):
-            level = max(top - n_red // ITERS, 0)
-            n_red += 1
+                st["level"] = max((st["level"] if st["level"] is not None else top) - 1, 0)
+            st["n_red"] = None
+            if st["level"] == top and st["cur"]:
+                st["solves"].append(st["cur"])
+                st["cur"] = []
+        elif st["n_red"] is not None and st["level"] is not None and name.startswith(("ic_reduce", "ic_split")):
+            st["level"] = max(top - st["n_red"] // ITERS, 0)
+            st["n_red"] += 1
+        level = st["level"]
         if level is None:
             continue
         layout = "nchw" if name.endswith("false>") else "c4"
+        mode = "solo" if sid == solo_stream else "side streams"
         if name.startswith(("ic_reduce", "ic_split", "finalize", "minmax")):
-            groups[(layout if not name.startswith(("finalize", "minmax")) else "-", level, name)].append(dur)
-        cur.append((int(r["Start_Timestamp"]), dur, level, name, int(r["Grid_Size_X"]) // max(int(r["Workgroup_Size_X"]), 1)))
-    # one channel-quad solve: the last complete one whose reduce launches are channel-quad
+            groups[(mode, layout if not name.startswith(("finalize", "minmax")) else "-", level, name)].append(dur)
+        st["cur"].append((int(r["Start_Timestamp"]), dur, level, name,
+                          int(r["Grid_Size_X"]) // max(int(r["Workgroup_Size_X"]), 1)))
+    for st in state.values():
+        if st["cur"]:
+            st["solves"].append(st["cur"])
+    # one channel-quad solve with nothing else in flight: the last solo one
+    solves = state[solo_stream]["solves"]
     c4 = [s for s in solves if any(n.endswith("true>") or n.startswith("ic_split") for _, _, _, n, _ in s)]
     one = c4[-1] if c4 else []
     # cut after the level-0 iterations of the solve (bench.py times extra level-0 launches after it)
@@ -82,14 +95,18 @@ def main():
     one = one[:cut]
     out = {"levels": {}, "timeline": []}
     lines = [f"# {a.title}\n" if a.title else "", "## Launches per level (all solves in the trace)\n",
-             "| layout | level | kernel | launches | avg us | min us | max us |", "|---|---|---|---|---|---|---|"]
-    for (layout, lv, name), d in sorted(groups.items(), key=lambda kv: (kv[0][0], -kv[0][1], kv[0][2])):
-        lines.append(f"| {layout} | {lv} | {name} | {len(d)} | {sum(d) / len(d):.1f} | {min(d):.1f} | {max(d):.1f} |")
-        out["levels"][f"{layout}/L{lv}/{name}"] = {"launches": len(d), "avg_us": sum(d) / len(d),
-                                                   "min_us": min(d), "max_us": max(d)}
+             "solo = default stream, nothing else in flight (warm-ups, latency loop, the roofline's level-0 "
+             "group); side streams = the timed region's graph replays, in flight together (launches overlap), plus "
+             "each slot's one eager pre-capture solve\n",
+             "| mode | layout | level | kernel | launches | avg us | min us | max us |",
+             "|---|---|---|---|---|---|---|---|"]
+    for (mode, layout, lv, name), d in sorted(groups.items(), key=lambda kv: (kv[0][0] != "solo", kv[0][1], -kv[0][2], kv[0][3])):
+        lines.append(f"| {mode} | {layout} | {lv} | {name} | {len(d)} | {sum(d) / len(d):.1f} | {min(d):.1f} | {max(d):.1f} |")
+        out["levels"][f"{mode}/{layout}/L{lv}/{name}"] = {"launches": len(d), "avg_us": sum(d) / len(d),
+                                                          "min_us": min(d), "max_us": max(d)}
     if one:
         t0 = one[0][0]
-        lines += ["", "## One channel-quad solve (B = 8 pairs, graph replay)\n",
+        lines += ["", "## One channel-quad solve (B = 8 pairs, graph replay, nothing else in flight)\n",
                   "| start us | duration us | level | kernel | workgroups |", "|---|---|---|---|---|"]
         for st, d, lv, name, wg in one:
             lines.append(f"| {(st - t0) / 1e3:.1f} | {d:.1f} | {lv} | {name} | {wg} |")
