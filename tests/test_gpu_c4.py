@@ -361,3 +361,47 @@ def test_pyramid_solver_iterate_uses_ready_extrema():
                                  d["sigma0"], d["sigma1"], first=True, remove_tru_sigma=True)
     torch.cuda.synchronize()
     assert torch.equal(Ra, Rb) and torch.equal(ta, tb.reshape(-1, 3))
+
+
+@pytest.mark.gpu
+def test_inflight_solves_bit_identical():
+    """bench.py --inflight: independent batches solved concurrently on separate streams,
+    each with its own PyramidSolver (workspace) and pose buffers, give exactly the poses
+    each gives alone (no shared state but the read-only inputs)."""
+    from deep_prob_feature_track_amd import ic
+    dev = _dev()
+    case, z = golden_io.load("cfg2_640x480_c32")
+    lv = golden_io.levels_torch(case, torch.float32, dev)
+    R0, t0 = golden_io.init_pose(case, torch.float32, dev)
+    K = torch.from_numpy(case["K"]).to(dev)
+    B, S = 8, 3
+    rep = lambda x: x.repeat(B, *([1] * (x.dim() - 1)))
+    levels = [dict(x0=rep(ic.pack_features(d["f0"])), x1=rep(ic.pack_features(d["f1"])), invD0=rep(d["invD0"]),
+                   invD1=rep(d["invD1"]), sigma0=rep(d["s0"]), sigma1=rep(d["s1"])) for d in lv]
+    # slot j starts from its own initial translations: distinct solves over shared inputs
+    inits = []
+    for j in range(S):
+        t = rep(t0.reshape(-1, 3)).clone()
+        t += 1e-3 * (j + 1) * torch.arange(B, device=dev, dtype=torch.float32).view(B, 1) / B
+        inits.append((rep(R0).contiguous(), t.contiguous()))
+    solvers = [ic.PyramidSolver(levels, rep(K), iters=3, remove_tru_sigma=True) for _ in range(S)]
+    alone = []
+    for j in range(S):
+        R, t = inits[j][0].clone(), inits[j][1].clone()
+        solvers[j].run(R, t)
+        torch.cuda.synchronize()
+        alone.append((R, t))
+    streams = [torch.cuda.Stream(dev) for _ in range(S)]
+    poses = [(inits[j][0].clone(), inits[j][1].clone()) for j in range(S)]
+    torch.cuda.synchronize()
+    for _ in range(4):
+        for j in range(S):
+            with torch.cuda.stream(streams[j]):
+                poses[j][0].copy_(inits[j][0])
+                poses[j][1].copy_(inits[j][1])
+                solvers[j].run(*poses[j])
+        torch.cuda.synchronize()
+        for j in range(S):
+            ic.check_status(solvers[j].status)
+            assert torch.equal(poses[j][0], alone[j][0]) and torch.equal(poses[j][1], alone[j][1])
+    assert not torch.equal(alone[0][1], alone[1][1])
