@@ -111,6 +111,32 @@ def copy_peak_gbs(device, nbytes=1 << 30, reps=5):
     return gbs
 
 
+def read_peak_gbs(device, nbytes, reps=10):
+    """Measured HBM read ceiling: the library's diagnostic streaming read
+    (dpft_read_probe: 16-byte loads, four in flight per lane, 4096 workgroups) over a
+    buffer of the level-0 launch's algorithmic size, plain and non-temporal loads;
+    returns the faster, in GB/s."""
+    import ctypes
+    from deep_prob_feature_track_amd import _native as N, ic
+    L = N.lib()
+    buf = torch.ones(nbytes // 4, dtype=torch.float32, device=device)
+    out = torch.empty(int(L.dpft_read_probe_out_floats()), dtype=torch.float32, device=device)
+    st = ctypes.c_void_p(torch.cuda.current_stream(device).cuda_stream)
+    best = 0.0
+    for nt in (0, 1):
+        for _ in range(3):
+            N.check(L.dpft_read_probe(ic._ptr(buf), buf.numel() * 4, nt, ic._ptr(out), st), "read probe")
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        for _ in range(reps):
+            N.check(L.dpft_read_probe(ic._ptr(buf), buf.numel() * 4, nt, ic._ptr(out), st), "read probe")
+        e1.record()
+        torch.cuda.synchronize()
+        best = max(best, buf.numel() * 4 * reps / (e0.elapsed_time(e1) * 1e-3) / 1e9)
+    del buf, out
+    return best
+
+
 def cpu_model():
     try:
         for line in open("/proc/cpuinfo"):
@@ -336,6 +362,7 @@ def main():
     achieved = alg_bytes / (kern_us * 1e-6) / 1e9
     traffic = l0_traffic() if a.layout == "c4" and B == 8 else None
     copy_gbs = copy_peak_gbs(device) if rank == 0 else None
+    read_gbs = read_peak_gbs(device, alg_bytes) if rank == 0 else None
 
     # secondary (rank 0 only, not the headline): the same solve from the other resident
     # layout, and the one-time cost of packing NCHW pyramids into the channel-quad layout
@@ -389,7 +416,9 @@ def main():
                          "kernel": f"ic_reduce_kernel<32,Cs=1,tru,U_IC,{a.layout}> (level 0, + in-kernel finalize)",
                          "kernel_us": kern_us, "algorithmic_bytes_per_launch": alg_bytes,
                          "measured_copy_peak": copy_gbs,
-                         "frac_of_measured_copy_peak": achieved / copy_gbs if copy_gbs else None},
+                         "frac_of_measured_copy_peak": achieved / copy_gbs if copy_gbs else None,
+                         "measured_read_peak": read_gbs,
+                         "frac_of_measured_read_peak": achieved / read_gbs if read_gbs else None},
             "cpu_baseline": cpu,
             "other_layout": other,
         }

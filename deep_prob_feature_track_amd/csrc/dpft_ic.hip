@@ -3267,9 +3267,52 @@ int sigma_extrema_impl(const DpftLevelDesc* descs, const DpftLevelTensors* tenso
                      static_cast<uint32_t*>(workspace));
   return hip_check("minmax_levels_kernel");
 }
+// Diagnostic streaming read (dpft_read_probe): every 16-byte word of a buffer once,
+// kProbeDepth loads in flight per lane, one float per wave written.  The measured HBM read
+// ceiling bench.py reports beside the roofline's spec peak.
+#ifndef DPFT_PROBE_GRID
+#define DPFT_PROBE_GRID 4096
+#endif
+#ifndef DPFT_PROBE_DEPTH
+#define DPFT_PROBE_DEPTH 4
+#endif
+constexpr int kProbeGrid = DPFT_PROBE_GRID;    // 16 workgroups per CU
+constexpr int kProbeDepth = DPFT_PROBE_DEPTH;  // 16-byte loads in flight per lane
+template <bool NT>
+__global__ __launch_bounds__(kThreads) void read_probe_kernel(const f32x4* __restrict__ p, size_t n4, float* out) {
+  const size_t stride = (size_t)gridDim.x * kThreads;
+  size_t i = (size_t)blockIdx.x * kThreads + threadIdx.x;
+  auto ld = [&](size_t k) { return NT ? __builtin_nontemporal_load(p + k) : p[k]; };
+  f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+  for (; i + (kProbeDepth - 1) * stride < n4; i += kProbeDepth * stride) {
+    f32x4 v[kProbeDepth];
+#pragma unroll
+    for (int k = 0; k < kProbeDepth; ++k) v[k] = ld(i + k * stride);
+#pragma unroll
+    for (int k = 0; k < kProbeDepth; ++k) acc += v[k];
+  }
+  for (; i < n4; i += stride) acc += ld(i);
+  float v = (acc.x + acc.y) + (acc.z + acc.w);
+  for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off);
+  if ((threadIdx.x & 63) == 0) out[blockIdx.x * (kThreads / 64) + (threadIdx.x >> 6)] = v;
+}
 }  // namespace
 
 extern "C" {
+
+size_t dpft_read_probe_out_floats(void) { return (size_t)kProbeGrid * (kThreads / 64); }
+
+int dpft_read_probe(const void* buf, size_t bytes, int32_t nontemporal, float* out, void* hip_stream) {
+  if (!buf || !out) return fail(DPFT_E_INVALID, "null pointer");
+  if (bytes < 16 || (reinterpret_cast<uintptr_t>(buf) & 15)) return fail(DPFT_E_INVALID, "need >= 16 aligned bytes");
+  const f32x4* p = static_cast<const f32x4*>(buf);
+  hipStream_t st = static_cast<hipStream_t>(hip_stream);
+  if (nontemporal)
+    hipLaunchKernelGGL(read_probe_kernel<true>, dim3(kProbeGrid), dim3(kThreads), 0, st, p, bytes / 16, out);
+  else
+    hipLaunchKernelGGL(read_probe_kernel<false>, dim3(kProbeGrid), dim3(kThreads), 0, st, p, bytes / 16, out);
+  return hip_check("read_probe_kernel");
+}
 
 size_t dpft_preprocess_workspace_size(void) { return kCtrlBytes; }
 

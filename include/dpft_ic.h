@@ -249,6 +249,16 @@ int dpft_preprocess_depth(const float* depth, int32_t B, int32_t H, int32_t W, i
  */
 int dpft_pack_features(const float* src, float* dst, int32_t B, int32_t C, int32_t H, int32_t W, void* hip_stream);
 
+/*
+ * Diagnostic, not on the solve path: read `bytes` (16-byte aligned) of device memory
+ * once with 16-byte loads (non-temporal if `nontemporal`), four in flight per lane,
+ * 4096 workgroups; writes dpft_read_probe_out_floats() partial sums to `out`.  Timed by
+ * bench.py as the measured HBM read ceiling the level-0 roofline is reported against
+ * beside the 8 TB/s spec.
+ */
+size_t dpft_read_probe_out_floats(void);
+int dpft_read_probe(const void* buf, size_t bytes, int32_t nontemporal, float* out, void* hip_stream);
+
 int dpft_version(void);            /* DPFT_ABI_VERSION */
 const char* dpft_last_error(void); /* thread-local message of the last failure */
 
