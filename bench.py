@@ -4,7 +4,7 @@
 One *step* = one full coarse-to-fine solve (levels 3..0, 3 Gauss-Newton
 iterations each = 12 IC iterations per pair) of a batch of B frame pairs per
 GPU, replayed from one HIP graph, followed (N > 1) by the RCCL all-gather of
-the per-pair poses.  An eval stream keeps --inflight batches (default 3, distinct
+the per-pair poses.  An eval stream keeps --inflight batches (default 4, distinct
 pairs each) in flight per GPU: step k replays slot k % inflight's graph on that
 slot's stream, so one batch's latency-bound coarse levels overlap another's
 bandwidth-bound level 0; every batch is solved exactly as alone (batch-global
@@ -40,7 +40,7 @@ def parse():
     p.add_argument("--steps", type=int, default=100)
     p.add_argument("--warmup", type=int, default=10)
     p.add_argument("--batch-per-gpu", type=int, default=8)
-    p.add_argument("--inflight", type=int, default=3,
+    p.add_argument("--inflight", type=int, default=4,
                    help="independent B-pair batches in flight per GPU (one stream, graph, workspace and input "
                         "set each; each batch's solve is unchanged, bit for bit)")
     p.add_argument("--kernel-reps", type=int, default=50)
