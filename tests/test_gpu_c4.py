@@ -304,12 +304,13 @@ def test_pyramid_solver_extrema_prepass_bit_identical(packed):
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("no_unc", [False, True])
-@pytest.mark.parametrize("B", [1, 8])
+@pytest.mark.parametrize("B", [1, 8, 64])
 def test_pyramid_entry_point(B, no_unc):
     """dpft_ic_solve_pyramid (the level loop of LeastSquareTracking.forward in one C call)
     against one dpft_ic_solve_level call per level: the same launches, bit for bit, and
-    on the golden case the reference's own poses.  B = 8: the bench's batch (replicated
-    golden pair); B = 1."""
+    on the golden case the reference's own poses.  B = 8: the bench's batch, B = 64: the
+    cfg3 batch on one GPU (the golden pair replicated: the batch-global extrema equal the
+    pair's own, so every pair must land on the reference's B = 1 poses); B = 1."""
     from deep_prob_feature_track_amd import ic
     dev = _dev()
     case, z = golden_io.load("cfg2_640x480_c32")
