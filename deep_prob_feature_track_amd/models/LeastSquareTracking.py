@@ -153,18 +153,29 @@ class LeastSquareTracking(nn.Module):
         # weights are the next level's prior (375-445) -- read by the IC tracker's learned
         # M-estimator, unused by the U_IC solver (its estimator call is commented out)
         wPrior = torch.ones_like(inv_d0[3]) * 0.001
-        for l in (3, 2, 1, 0):
-            tr = getattr(self, f'tr_update{l}')
-            Kl = K / float(1 << l)
-            if self.track_type == 'IC':
-                out = tr(pose, x0[l], x1[l], inv_d0[l], inv_d1[l], Kl, wPrior, vis_res=False,
-                         obj_mask0=m0[l], obj_mask1=m1[l])
-                wPrior = out[1]
-            else:
-                out = tr(pose, x0[l], x1[l], inv_d0[l], inv_d1[l], Kl, sigma0=sigma0[l], sigma1=sigma1[l],
-                         wPrior=None, vis_res=False, depth0=dpt0[l], depth1=dpt1[l], obj_mask0=m0[l],
-                         obj_mask1=m1[l])
-            pose = out[0]
+        # U_IC: the four levels share one status word, read once after the finest level
+        # (the reference asserts per iteration; either way a non-finite Jacobian or
+        # residual raises AssertionError out of forward and no pose is returned)
+        status = torch.zeros(1, dtype=torch.int32, device=x0[0].device) if self.track_type != 'IC' else None
+        try:
+            for l in (3, 2, 1, 0):
+                tr = getattr(self, f'tr_update{l}')
+                Kl = K / float(1 << l)
+                if self.track_type == 'IC':
+                    out = tr(pose, x0[l], x1[l], inv_d0[l], inv_d1[l], Kl, wPrior, vis_res=False,
+                             obj_mask0=m0[l], obj_mask1=m1[l])
+                    wPrior = out[1]
+                else:
+                    tr._deferred_status = status
+                    out = tr(pose, x0[l], x1[l], inv_d0[l], inv_d1[l], Kl, sigma0=sigma0[l], sigma1=sigma1[l],
+                             wPrior=None, vis_res=False, depth0=dpt0[l], depth1=dpt1[l], obj_mask0=m0[l],
+                             obj_mask1=m1[l])
+                pose = out[0]
+        finally:
+            for l in (3, 2, 1, 0):
+                getattr(self, f'tr_update{l}')._deferred_status = None
+        if status is not None:
+            ic.check_status(status)
         return pose
 
     def compute_residual(self, img0, img1, depth0, depth1, K, poseI=None, level_i=0, logger=None, vis=False,
@@ -255,7 +266,9 @@ class LeastSquareTracking(nn.Module):
                     R0, t0 = self.pose_predictor(orig_x0[3], orig_x1[3])
             else:
                 B = invD0.shape[0]
-                R0 = torch.eye(3, dtype=torch.float).expand(B, 3, 3).type_as(I0)
-                t0 = torch.zeros(B, 3, 1, dtype=torch.float).type_as(I0)
+                # made on the device (the reference builds them on the host and copies,
+                # 693-695: a synchronous copy that stalls the host behind the encoder)
+                R0 = torch.eye(3, dtype=I0.dtype, device=I0.device).expand(B, 3, 3)
+                t0 = torch.zeros(B, 3, 1, dtype=I0.dtype, device=I0.device)
             poseI = [R0, t0]
         return (I0, I1, x0, x1, sigma0, sigma1, dpt0, dpt1, inv_d0, inv_d1, m0, m1, poseI)

@@ -60,8 +60,10 @@ class FeaturePyramid(nn.Module):
     """Four-scale feature + uncertainty encoder (algorithms.py:1221-1430).
 
     Returns (features [4], sigmas [4], backbone maps [4]); a 1-channel uncertainty
-    is repeated to the feature channels as in the reference (1426-1427) -- the
-    solver wrapper recognises the repeat and hands the kernel one plane."""
+    is repeated to the feature channels as in the reference (1426-1427), as a
+    channel-broadcast view (same shape and values, no copy) that the solver wrapper
+    recognises and hands to the kernel as one plane (Cs = 1: 2 sigma planes of reads
+    per pixel instead of 2C)."""
 
     def __init__(self, D, w_uncertainty='None', feature_channel=1, feature_extract='conv', uncertainty_channel=1):
         super().__init__()
@@ -136,7 +138,7 @@ class FeaturePyramid(nn.Module):
         if self.uncertainty_type != 'feature':
             sigma = [_UNCERTAINTY_ACTIVATIONS[self.uncertainty_type](si) for si in sigma]
         if self.uncertainty_C == 1 and self.output_C != 1:
-            sigma = [si.repeat((1, self.output_C, 1, 1)) for si in sigma]
+            sigma = [si.expand(-1, self.output_C, -1, -1) for si in sigma]
         return f, sigma, maps
 
 
@@ -460,6 +462,10 @@ class TrustRegionInverseWUncertainty(nn.Module):
     def __init__(self, max_iter=3, mEst_func=None, solver_func=None, timers=None, uncer_prop=False,
                  combine_icp=False, scale_func=None, remove_tru_sigma=False):
         super().__init__()
+        # a [1] int32 device word set by LeastSquareTracking.forward for one pyramid
+        # solve: the levels OR their non-finite flag into it and the driver checks it once
+        # (one host read per forward instead of one per level); None = check every call
+        self._deferred_status = None
         self.max_iterations = max_iter
         self.mEstimator = mEst_func
         self.directSolver = solver_func
@@ -491,9 +497,10 @@ class TrustRegionInverseWUncertainty(nn.Module):
         self._check_path(x0)
         B, C, H, W = x0.shape
         kw = self._common(x0, depth0, depth1, obj_mask0, obj_mask1)
+        st = self._deferred_status
         with torch.no_grad():
             out = ic.solve_level(pose10, x0, x1, invD0, invD1, K, sigma0, sigma1, iters=self.max_iterations,
-                                 return_jtj=self.uncer_prop, **kw)
+                                 return_jtj=self.uncer_prop, check=st is None, status=st, **kw)
         pose = [out[0], out[1]]
         if self.combine_icp:
             weights = torch.full((1, 1, 1, 1), self._icp_scale(), dtype=x0.dtype, device=x0.device).expand(B, 1, H, W)

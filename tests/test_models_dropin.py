@@ -102,6 +102,25 @@ def test_forward_and_residual_match_reference(name):
 
 
 @pytest.mark.gpu
+def test_forward_nonfinite_raises_assertion_and_module_recovers():
+    """A NaN input pixel makes the Jacobian / residual non-finite: forward raises
+    AssertionError like the reference's `assert check_nan(...) == 0` (algorithms.py:886,
+    1988) -- the four levels share one status word read once per forward -- and the
+    module then solves finite inputs exactly as before (no stale status)."""
+    m, T = _loaded("convrgbd2_c8", "cuda")
+    with torch.no_grad():
+        R0, t0 = m(T["img0"], T["img1"], T["depth0"], T["depth1"], T["K"])
+        bad = T["img0"].clone()
+        bad[:, :, 40:44, 60:64] = float("nan")
+        with pytest.raises(AssertionError):
+            m(bad, T["img1"], T["depth0"], T["depth1"], T["K"])
+        assert all(getattr(m, f"tr_update{l}")._deferred_status is None for l in range(4))
+        R1, t1 = m(T["img0"], T["img1"], T["depth0"], T["depth1"], T["K"])
+    # the encoder (MIOpen) is not bit-reproducible from call to call; the solver is
+    assert (R0 - R1).abs().max().item() < 1e-5 and (t0 - t1).abs().max().item() < 1e-5
+
+
+@pytest.mark.gpu
 @pytest.mark.parametrize("name", ["convrgbd2_c8", "convrgbd2_c8_icp", "rgb_identity_masks", "convrgbd_c8_ic_masks"])
 def test_convergence_basin_landscape_matches_reference(name):
     """The multi-pose residual sweep equals the reference's one-compute_residual-per-pose

@@ -1,0 +1,64 @@
+"""Time the drop-in `LeastSquareTracking.forward` on the GPU at the bench's shape
+(B = 8, 640x480, C = 32, Cs = 1, ConvRGBD2 / laplacian, remove_tru_sigma; random
+encoder weights): the whole forward, its `_preprocess` (encoder, pyramids, depth) and
+the solver levels (forward minus preprocess).
+
+python tools/dropin_timing.py [--reps 20]
+"""
+import argparse
+import os
+import sys
+import time
+
+import torch
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path[:0] = [ROOT, os.path.join(ROOT, "tests", "golden")]
+import recipe  # noqa: E402
+from deep_prob_feature_track_amd.models.LeastSquareTracking import LeastSquareTracking, default_options  # noqa: E402
+
+ap = argparse.ArgumentParser()
+ap.add_argument("--reps", type=int, default=20)
+ap.add_argument("--batch", type=int, default=8)
+a = ap.parse_args()
+dev = torch.device("cuda:0")
+if os.environ.get("DPFT_DROPIN_BENCHMARK"):  # MIOpen algorithm search for the encoder convs
+    torch.backends.cudnn.benchmark = True
+torch.manual_seed(0)
+m = LeastSquareTracking("ConvRGBD2", "laplacian", 3, "None", "Direct-Nodamping",
+                        options=default_options(feature_channel=32, uncertainty_channel=1, feature_extract="conv",
+                                                remove_tru_sigma=True)).to(dev).eval()
+B = a.batch
+pairs = [(i % 5, (i + 1 + i // 5) % 5) for i in range(B)]
+img0 = torch.stack([torch.from_numpy(recipe.color_float(i, 1)) for i, _ in pairs]).to(dev)
+img1 = torch.stack([torch.from_numpy(recipe.color_float(j, 1)) for _, j in pairs]).to(dev)
+d0 = torch.stack([torch.from_numpy(recipe.depth_m(i, 1)) for i, _ in pairs])[:, None].to(dev)
+d1 = torch.stack([torch.from_numpy(recipe.depth_m(j, 1)) for _, j in pairs])[:, None].to(dev)
+K = torch.tensor(recipe.K_FULL, device=dev).view(1, 4).repeat(B, 1)
+
+
+def timed(fn):
+    with torch.no_grad():
+        for _ in range(3):
+            fn()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(a.reps):
+            fn()
+        torch.cuda.synchronize()
+    return (time.perf_counter() - t0) / a.reps * 1e3
+
+
+full = timed(lambda: m.forward(img0, img1, d0, d1, K))
+pre = timed(lambda: m._preprocess(img0, img1, d0, d1))
+print(f"drop-in forward B={B} 640x480 C=32: {full:.2f} ms per call; _preprocess {pre:.2f} ms; "
+      f"solver levels {full - pre:.2f} ms", flush=True)
+
+if os.environ.get("DPFT_DROPIN_PROFILE"):
+    from torch.profiler import ProfilerActivity, profile
+    with torch.no_grad(), profile(activities=[ProfilerActivity.CPU, ProfilerActivity.CUDA]) as prof:
+        for _ in range(3):
+            m.forward(img0, img1, d0, d1, K)
+        torch.cuda.synchronize()
+    print(prof.key_averages().table(sort_by="cuda_time_total", row_limit=25), flush=True)
+    print(prof.key_averages().table(sort_by="cpu_time_total", row_limit=25), flush=True)
