@@ -45,8 +45,8 @@ class LevelTensors(ctypes.Structure):
 EXPORTS = ("dpft_workspace_size", "dpft_ic_solve_level", "dpft_ic_solve_pyramid", "dpft_ic_iterate", "dpft_ic_residual_level",
            "dpft_residual_poses_workspace_size", "dpft_ic_residual_poses", "dpft_ic_residual_map",
            "dpft_ic_reduce_only", "dpft_ic_debug_pixels", "dpft_preprocess_workspace_size",
-           "dpft_preprocess_depth", "dpft_pack_features", "dpft_sigma_extrema_levels", "dpft_read_probe_out_floats",
-           "dpft_read_probe", "dpft_version", "dpft_last_error")
+           "dpft_preprocess_depth", "dpft_pack_features", "dpft_sigma_extrema_levels", "dpft_ic_damped_update",
+           "dpft_read_probe_out_floats", "dpft_read_probe", "dpft_version", "dpft_last_error")
 
 _lib = None
 
@@ -90,6 +90,8 @@ def lib():
     L.dpft_sigma_extrema_levels.restype = ctypes.c_int
     L.dpft_pack_features.argtypes = [vp, vp, ctypes.c_int32, ctypes.c_int32, ctypes.c_int32, ctypes.c_int32, vp]
     L.dpft_pack_features.restype = ctypes.c_int
+    L.dpft_ic_damped_update.argtypes = [vp, vp, vp, ctypes.c_int32, ctypes.c_int32, vp, vp, vp, vp, vp]
+    L.dpft_ic_damped_update.restype = ctypes.c_int
     L.dpft_read_probe_out_floats.argtypes = []
     L.dpft_read_probe_out_floats.restype = sz
     L.dpft_read_probe.argtypes = [vp, sz, ctypes.c_int32, vp, vp]

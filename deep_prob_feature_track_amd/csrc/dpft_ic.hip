@@ -781,7 +781,12 @@ __device__ __forceinline__ double rsqrt_d(double x) {
 // reference's batched inverse) and apply the inverse-compositional update
 // (algorithms.py:2035-2054, geometry.py:105-123, 163-185):
 // R <- R Exp(-w), t <- R (-Exp(-w) v) + t.
-__device__ void solve_and_update(const double* jtj_u, const double* jtr, float* Rp, float* tp) {
+// `diag_add` (optional): extra damping on the diagonal, H = JtJ + diag(diag_add) +
+// 1e-6 tr(JtJ) I -- the residual-volume trial and learned-damping matrices of
+// 'Direct-ResVol' (algorithms.py:1664-1691); the 1e-6 tr term is the reference's
+// epsilon there and lev_mar_H's damping here.
+__device__ void solve_and_update(const double* jtj_u, const double* jtr, float* Rp, float* tp,
+                                 const double* diag_add = nullptr) {
 #if DPFT_ABL_SOLVE == 1  // profiling ablation: no solve / update
   return;
 #endif
@@ -797,7 +802,7 @@ __device__ void solve_and_update(const double* jtj_u, const double* jtr, float* 
     }
   const double tr = ((((A[0][0] + A[1][1]) + A[2][2]) + A[3][3]) + A[4][4]) + A[5][5];
 #pragma unroll
-  for (int i = 0; i < 6; ++i) A[i][i] += 1e-6 * tr;
+  for (int i = 0; i < 6; ++i) A[i][i] = (diag_add ? A[i][i] + diag_add[i] : A[i][i]) + 1e-6 * tr;
   double L[6][6], invd[6];
 #pragma unroll
   for (int j = 0; j < 6; ++j) {
@@ -3267,6 +3272,33 @@ int sigma_extrema_impl(const DpftLevelDesc* descs, const DpftLevelTensors* tenso
                      static_cast<uint32_t*>(workspace));
   return hip_check("minmax_levels_kernel");
 }
+// One thread per (sample s, pair b): H = JtJ_b + diag(diag_add[s, b]) + 1e-6 tr(JtJ_b) I,
+// xi = H^-1 JtR_b (fp64 Cholesky), pose_out[s, b] = the inverse-compositional update of
+// pose_b (dpft_ic_damped_update).
+__global__ __launch_bounds__(kThreads) void damped_update_kernel(const float* __restrict__ jtj,
+                                                                 const float* __restrict__ jtr,
+                                                                 const float* __restrict__ diag_add, int S, int B,
+                                                                 const float* __restrict__ R,
+                                                                 const float* __restrict__ t, float* R_out,
+                                                                 float* t_out) {
+  const int i = blockIdx.x * kThreads + threadIdx.x;
+  if (i >= S * B) return;
+  const int b = i % B;
+  double ju[21], jr[6], dg[6];
+  int k = 0;
+  for (int r = 0; r < 6; ++r)
+    for (int c = r; c < 6; ++c) ju[k++] = jtj[36 * b + 6 * r + c];
+  for (int r = 0; r < 6; ++r) {
+    jr[r] = jtr[6 * b + r];
+    dg[r] = diag_add ? diag_add[6 * i + r] : 0.0;
+  }
+  float* Ro = R_out + 9 * (size_t)i;
+  float* to = t_out + 3 * (size_t)i;
+  for (int r = 0; r < 9; ++r) Ro[r] = R[9 * b + r];
+  for (int r = 0; r < 3; ++r) to[r] = t[3 * b + r];
+  solve_and_update(ju, jr, Ro, to, dg);
+}
+
 // Diagnostic streaming read (dpft_read_probe): every 16-byte word of a buffer once,
 // kProbeDepth loads in flight per lane, one float per wave written.  The measured HBM read
 // ceiling bench.py reports beside the roofline's spec peak.
@@ -3299,6 +3331,16 @@ __global__ __launch_bounds__(kThreads) void read_probe_kernel(const f32x4* __res
 }  // namespace
 
 extern "C" {
+
+int dpft_ic_damped_update(const float* jtj, const float* jtr, const float* diag_add, int32_t S, int32_t B,
+                          const float* R, const float* t, float* R_out, float* t_out, void* hip_stream) {
+  if (!jtj || !jtr || !R || !t || !R_out || !t_out) return fail(DPFT_E_INVALID, "null pointer");
+  if (S < 1 || B < 1 || (long)S * B > (1L << 24)) return fail(DPFT_E_INVALID, "bad S=%d B=%d", S, B);
+  const int n = S * B;
+  hipLaunchKernelGGL(damped_update_kernel, dim3((n + kThreads - 1) / kThreads), dim3(kThreads), 0,
+                     static_cast<hipStream_t>(hip_stream), jtj, jtr, diag_add, S, B, R, t, R_out, t_out);
+  return hip_check("damped_update_kernel");
+}
 
 size_t dpft_read_probe_out_floats(void) { return (size_t)kProbeGrid * (kThreads / 64); }
 

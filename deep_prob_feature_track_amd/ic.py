@@ -221,6 +221,47 @@ def iterate(pose, x0, x1, invD0, invD1, K, sigma0, sigma1, first=True, reverse=F
     return R, t.view(c.B, 3, 1), jtj, jtr, inv
 
 
+def iterate_poses(R, t, x0, x1, invD0, invD1, K, sigma0, sigma1, **kw):
+    """J^T J and J^T R at S poses per pair, no update: R [S,B,3,3], t [S,B,3(,1)] ->
+    (JtJ [S,B,6,6], JtR [S,B,6]).  One validated LevelCall (workspace, pointers) for all
+    S, then S dpft_ic_iterate calls with DPFT_ITER_NO_UPDATE on the current stream --
+    the residual-volume samples of 'Direct-ResVol' (algorithms.py:1668-1685)."""
+    c = LevelCall(x0, x1, invD0, invD1, K, sigma0, sigma1, iters=1, **kw)
+    S = R.shape[0]
+    R = R.to(torch.float32).reshape(S, c.B, 3, 3).contiguous()
+    t = t.to(torch.float32).reshape(S, c.B, 3).contiguous()
+    jtj = torch.empty(S, c.B, 6, 6, dtype=torch.float32, device=c.device)
+    jtr = torch.empty(S, c.B, 6, dtype=torch.float32, device=c.device)
+    st = _stream(c.device)
+    for s in range(S):
+        rc = N.lib().dpft_ic_iterate(ctypes.byref(c.desc), ctypes.byref(c.tens), _ptr(R[s]), _ptr(t[s]),
+                                     _ptr(jtj[s]), _ptr(jtr[s]), None, N.ITER_NO_UPDATE, _ptr(c.ws), c.ws_bytes, st)
+        N.check(rc, "dpft_ic_iterate")
+    return jtj, jtr
+
+
+def damped_update(JtJ, JtR, diag_add, pose):
+    """S damped inverse-compositional updates per pair in one launch (dpft_ic_damped_update):
+    JtJ [B,6,6], JtR [B,6], diag_add [S,B,6] or None (S = 1), pose ([B,3,3], [B,3(,1)])
+    -> (R [S,B,3,3], t [S,B,3,1])."""
+    R, t = pose
+    dev = JtJ.device
+    B = JtJ.shape[0]
+    jtj = JtJ.to(torch.float32).reshape(B, 36).contiguous()
+    jtr = JtR.to(torch.float32).reshape(B, 6).contiguous()
+    R = R.to(torch.float32).reshape(B, 9).contiguous()
+    t = t.to(torch.float32).reshape(B, 3).contiguous()
+    if diag_add is not None:
+        diag_add = diag_add.to(torch.float32).reshape(-1, B, 6).contiguous()
+    S = diag_add.shape[0] if diag_add is not None else 1
+    R_out = torch.empty(S, B, 3, 3, dtype=torch.float32, device=dev)
+    t_out = torch.empty(S, B, 3, 1, dtype=torch.float32, device=dev)
+    rc = N.lib().dpft_ic_damped_update(_ptr(jtj), _ptr(jtr), _ptr(diag_add), S, B, _ptr(R), _ptr(t), _ptr(R_out),
+                                       _ptr(t_out), _stream(dev))
+    N.check(rc, "dpft_ic_damped_update")
+    return R_out, t_out
+
+
 def residual_map(pose, x0, x1, invD0, invD1, K, **kw):
     """IC tracker residuals at `pose` (compute_warped_residual, algorithms.py:1919-1957):
     (r [B,C,H,W] with 1e-3 on occluded / masked pixels, occ [B,1,H,W] bool)."""

@@ -218,10 +218,12 @@ def _twist2mat(w):
 
 def inverse_update_pose(H, JtR, pose):
     """xi = H^-1 JtR, R <- R Exp(-w), t <- R (-Exp(-w) v) + t (algorithms.py:2017-2054),
-    batched on the device in fp64 (the reference inverts on the host CPU in fp32, 2077-2091)."""
+    batched on the device in fp64 (the reference inverts on the host CPU in fp32, 2077-2091).
+    `solve_ex`: no host read of the factorisation status (a singular H gives inf / NaN
+    poses, as the reference's inverse does)."""
     R, t = pose
     B = H.shape[0]
-    xi = torch.linalg.solve(H.double(), JtR.double().reshape(B, 6, 1)).view(B, 6)
+    xi = torch.linalg.solve_ex(H.double(), JtR.double().reshape(B, 6, 1))[0].view(B, 6)
     dR = _twist2mat(-xi[:, :3])
     dt = -torch.bmm(dR, xi[:, 3:].reshape(B, 3, 1))
     R1, t1 = geometry.batch_Rt_compose(R.double(), t.double(), dR, dt)
@@ -246,6 +248,7 @@ class DirectSolverNet(nn.Module):
             self.type = self.SOLVER_NO_DAMPING
         elif solver_type == 'Direct-ResVol':
             self.samples = samples
+            self._lambdas = None  # logspace(-5, 5, samples) on the device, made once
             self.net = deep_damping_regressor(D=6 * 6 + 6 * samples)
             self.type = self.SOLVER_RESIDUAL_VOLUME
             initialize_weights(self.net)
@@ -268,20 +271,18 @@ class DirectSolverNet(nn.Module):
                                        no_uncertainty=True, weights=weights, obj_mask0=obj_mask0,
                                        obj_mask1=obj_mask1)
         pose = [R, t]
-        diag_mask = torch.eye(6, dtype=JtJ.dtype, device=JtJ.device).view(1, 6, 6)
-        diagJtJ = diag_mask * JtJ
-        epsilon = (torch.sum(diagJtJ, (2, 1)) * 1e-6).view(B, 1, 1) * diag_mask
-        lambdas = torch.logspace(-5, 5, self.samples, dtype=JtJ.dtype, device=JtJ.device)
-        vols = []
-        for s in range(self.samples):
-            pose_s = inverse_update_pose(JtJ + lambdas[s] * diagJtJ + epsilon, JtR, pose)
-            _, _, _, JtR_s, _ = ic.iterate(pose_s, x0, x1, invD0, invD1, K, None, None, first=False, update=False,
-                                           no_uncertainty=True, weights=weights, obj_mask1=obj_mask1)
-            vols.append(JtR_s.view(B, 6, 1))
-        JtR_flat = torch.cat(vols, dim=2).view(B, -1)
+        S = self.samples
+        if self._lambdas is None or self._lambdas.device != JtJ.device:
+            self._lambdas = torch.logspace(-5, 5, S, dtype=torch.float32, device=JtJ.device).view(S, 1, 1)
+        # the S trial poses (JtJ + lambda_s diag(JtJ) + 1e-6 tr I) in one launch, their
+        # J^T W r through one LevelCall, the learned damping's update in one more launch
+        R_s, t_s = ic.damped_update(JtJ, JtR, self._lambdas * torch.diagonal(JtJ, dim1=1, dim2=2), pose)
+        _, JtR_s = ic.iterate_poses(R_s, t_s, x0, x1, invD0, invD1, K, None, None,
+                                    no_uncertainty=True, weights=weights, obj_mask1=obj_mask1)
+        JtR_flat = JtR_s.permute(1, 2, 0).reshape(B, -1)  # [B, 6, S]: as the reference's cat(dim=2)
         damp = self.net(torch.cat((JtR_flat, JtJ.view(B, -1)), dim=1))
-        H = JtJ + diag_mask * damp.view(B, 6, 1) + epsilon
-        return inverse_update_pose(H, JtR, pose)
+        R1, t1 = ic.damped_update(JtJ, JtR, damp.view(1, B, 6), pose)
+        return [R1[0], t1[0]]
 
 
 # ------------------------------------------------------------------ init-pose networks

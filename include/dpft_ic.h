@@ -250,6 +250,19 @@ int dpft_preprocess_depth(const float* depth, int32_t B, int32_t H, int32_t W, i
 int dpft_pack_features(const float* src, float* dst, int32_t B, int32_t C, int32_t H, int32_t W, void* hip_stream);
 
 /*
+ * Damped inverse-compositional update of 'Direct-ResVol' (DirectSolverNet,
+ * algorithms.py:1644-1691, then inverse_update_pose 2017-2054), for S damping choices
+ * per pair at once: H[s,b] = JtJ[b] + diag(diag_add[s,b]) + 1e-6 tr(JtJ[b]) I,
+ * xi = H^-1 JtR[b] (fp64 Cholesky), R_out[s,b] = R[b] Exp(-w), t_out[s,b] =
+ * R[b] (-Exp(-w) v) + t[b].  jtj [B,6,6], jtr [B,6], diag_add [S,B,6] (NULL: none),
+ * R [B,3,3], t [B,3] -> R_out [S,B,3,3], t_out [S,B,3]; outputs must not alias inputs.
+ * The residual-volume trial poses use diag_add = lambda_s diag(JtJ), the final step the
+ * MLP's damping.
+ */
+int dpft_ic_damped_update(const float* jtj, const float* jtr, const float* diag_add, int32_t S, int32_t B,
+                          const float* R, const float* t, float* R_out, float* t_out, void* hip_stream);
+
+/*
  * Diagnostic, not on the solve path: read `bytes` (16-byte aligned) of device memory
  * once with 16-byte loads (non-temporal if `nontemporal`), four in flight per lane,
  * 4096 workgroups; writes dpft_read_probe_out_floats() partial sums to `out`.  Timed by

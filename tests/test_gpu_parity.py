@@ -323,3 +323,58 @@ def test_ic_residual_map_and_weighted_normal_equations(B, C, H, W, masks, packed
                                      no_uncertainty=True, weights=cu(w), obj_mask0=cu(m0), obj_mask1=cu(m1))
     Ro, to, _ = O.damped_solve_update(jtj.cpu().double(), jtr.cpu().double().view(B, 6, 1), R.double(), t.double())
     assert (R1.cpu().double() - Ro).abs().max() < 1e-5 and (t1.cpu().double().view(B, 3) - to.view(B, 3)).abs().max() < 1e-5
+
+
+def test_damped_update_matches_fp64_reference_update():
+    """dpft_ic_damped_update (the ResVol trial poses and the learned-damping step in one
+    launch) against the fp64 PyTorch restatement of inverse_update_pose (algorithms.py:
+    2017-2054) with H = JtJ + diag(d) + 1e-6 tr(JtJ) I (1664-1691)."""
+    from deep_prob_feature_track_amd import ic
+    from deep_prob_feature_track_amd.models.algorithms import inverse_update_pose
+    dev = _dev()
+    g = torch.Generator().manual_seed(3)
+    S, B = 10, 5
+    A = torch.randn(B, 6, 40, generator=g, dtype=torch.float64)
+    JtJ = (A @ A.transpose(1, 2)).float()
+    JtR = (0.05 * torch.randn(B, 6, generator=g, dtype=torch.float64)).float()
+    ang = 0.3 * torch.randn(B, 3, generator=g, dtype=torch.float64)
+    from deep_prob_feature_track_amd.models.algorithms import _twist2mat
+    R = _twist2mat(ang).float()
+    t = torch.randn(B, 3, 1, generator=g).float()
+    lam = torch.logspace(-5, 5, S, dtype=torch.float32).view(S, 1, 1)
+    diag = lam * torch.diagonal(JtJ, dim1=1, dim2=2).unsqueeze(0)
+    Rs, ts = ic.damped_update(JtJ.to(dev), JtR.to(dev), diag.to(dev), [R.to(dev), t.to(dev)])
+    eye = torch.eye(6, dtype=torch.float64)
+    for s in range(S):
+        H = (JtJ.double() + torch.diag_embed(diag[s].double()) +
+             1e-6 * torch.diagonal(JtJ.double(), dim1=1, dim2=2).sum(1).view(B, 1, 1) * eye)
+        Rr, tr = inverse_update_pose(H, JtR.double(), [R.double(), t.double()])
+        assert (Rs[s].cpu().double() - Rr).abs().max().item() < 2e-6
+        assert (ts[s].cpu().double() - tr).abs().max().item() < 2e-6
+    # S = 1 without extra damping: lev_mar_H's matrix
+    R1, t1 = ic.damped_update(JtJ.to(dev), JtR.to(dev), None, [R.to(dev), t.to(dev)])
+    H = JtJ.double() + 1e-6 * torch.diagonal(JtJ.double(), dim1=1, dim2=2).sum(1).view(B, 1, 1) * eye
+    Rr, tr = inverse_update_pose(H, JtR.double(), [R.double(), t.double()])
+    assert (R1[0].cpu().double() - Rr).abs().max().item() < 2e-6 and (t1[0].cpu().double() - tr).abs().max() < 2e-6
+
+
+def test_iterate_poses_equals_per_pose_iterate():
+    """ic.iterate_poses (one LevelCall, S no-update iterations) against S separate
+    ic.iterate(update=False) calls: the same launches, bit for bit."""
+    from deep_prob_feature_track_amd import ic
+    dev = _dev()
+    case, z = golden_io.load("cfg1_160x120_c8")
+    lv = golden_io.levels_torch(case, torch.float32, dev)[0]
+    R0, t0 = golden_io.init_pose(case, torch.float32, dev)
+    K = torch.from_numpy(case["K"]).to(dev)
+    S = 4
+    B = R0.shape[0]
+    Rs = torch.stack([R0.reshape(B, 3, 3)] * S).contiguous()
+    ts = torch.stack([t0.reshape(B, 3) + 0.01 * s for s in range(S)]).contiguous()
+    w = torch.rand(B, 1, *lv["f0"].shape[2:], device=dev) + 0.5
+    kw = dict(no_uncertainty=True, weights=w)
+    jtj, jtr = ic.iterate_poses(Rs, ts, lv["f0"], lv["f1"], lv["invD0"], lv["invD1"], K, None, None, **kw)
+    for s in range(S):
+        _, _, jtj1, jtr1, _ = ic.iterate((Rs[s], ts[s].view(B, 3, 1)), lv["f0"], lv["f1"], lv["invD0"], lv["invD1"], K,
+                                         None, None, first=False, update=False, **kw)
+        assert torch.equal(jtj[s], jtj1) and torch.equal(jtr[s], jtr1)

@@ -20,21 +20,29 @@ from deep_prob_feature_track_amd.models.LeastSquareTracking import LeastSquareTr
 ap = argparse.ArgumentParser()
 ap.add_argument("--reps", type=int, default=20)
 ap.add_argument("--batch", type=int, default=8)
+ap.add_argument("--config", default="uic", choices=["uic", "deepic"],
+                help="uic: ConvRGBD2 + laplacian U_IC tracker, C=32; deepic: RGB features, IC tracker, "
+                     "MultiScale2w M-estimator, Direct-ResVol")
+ap.add_argument("--down", type=int, default=1, help="image subsampling (1: 640x480)")
 a = ap.parse_args()
 dev = torch.device("cuda:0")
 if os.environ.get("DPFT_DROPIN_BENCHMARK"):  # MIOpen algorithm search for the encoder convs
     torch.backends.cudnn.benchmark = True
 torch.manual_seed(0)
-m = LeastSquareTracking("ConvRGBD2", "laplacian", 3, "None", "Direct-Nodamping",
-                        options=default_options(feature_channel=32, uncertainty_channel=1, feature_extract="conv",
-                                                remove_tru_sigma=True)).to(dev).eval()
+if a.config == "uic":
+    m = LeastSquareTracking("ConvRGBD2", "laplacian", 3, "None", "Direct-Nodamping",
+                            options=default_options(feature_channel=32, uncertainty_channel=1, feature_extract="conv",
+                                                    remove_tru_sigma=True)).to(dev).eval()
+else:
+    m = LeastSquareTracking("RGB", "None", 3, "MultiScale2w", "Direct-ResVol",
+                            options=default_options(feature_channel=1)).to(dev).eval()
 B = a.batch
 pairs = [(i % 5, (i + 1 + i // 5) % 5) for i in range(B)]
-img0 = torch.stack([torch.from_numpy(recipe.color_float(i, 1)) for i, _ in pairs]).to(dev)
-img1 = torch.stack([torch.from_numpy(recipe.color_float(j, 1)) for _, j in pairs]).to(dev)
-d0 = torch.stack([torch.from_numpy(recipe.depth_m(i, 1)) for i, _ in pairs])[:, None].to(dev)
-d1 = torch.stack([torch.from_numpy(recipe.depth_m(j, 1)) for _, j in pairs])[:, None].to(dev)
-K = torch.tensor(recipe.K_FULL, device=dev).view(1, 4).repeat(B, 1)
+img0 = torch.stack([torch.from_numpy(recipe.color_float(i, a.down)) for i, _ in pairs]).to(dev)
+img1 = torch.stack([torch.from_numpy(recipe.color_float(j, a.down)) for _, j in pairs]).to(dev)
+d0 = torch.stack([torch.from_numpy(recipe.depth_m(i, a.down)) for i, _ in pairs])[:, None].to(dev)
+d1 = torch.stack([torch.from_numpy(recipe.depth_m(j, a.down)) for _, j in pairs])[:, None].to(dev)
+K = torch.tensor(recipe.K_FULL / a.down, device=dev).view(1, 4).repeat(B, 1)
 
 
 def timed(fn):
@@ -51,7 +59,8 @@ def timed(fn):
 
 full = timed(lambda: m.forward(img0, img1, d0, d1, K))
 pre = timed(lambda: m._preprocess(img0, img1, d0, d1))
-print(f"drop-in forward B={B} 640x480 C=32: {full:.2f} ms per call; _preprocess {pre:.2f} ms; "
+H, W = img0.shape[2:]
+print(f"drop-in forward ({a.config}) B={B} {W}x{H}: {full:.2f} ms per call; _preprocess {pre:.2f} ms; "
       f"solver levels {full - pre:.2f} ms", flush=True)
 
 if os.environ.get("DPFT_DROPIN_PROFILE"):
