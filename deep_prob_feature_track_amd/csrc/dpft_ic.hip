@@ -3272,6 +3272,132 @@ int sigma_extrema_impl(const DpftLevelDesc* descs, const DpftLevelTensors* tenso
                      static_cast<uint32_t*>(workspace));
   return hip_check("minmax_levels_kernel");
 }
+// ---------------------------------------------------------------------------------
+// Jacobian API, materialised (the reference's solver methods precompute_jacobian_
+// components / compose_inverse_jacobians / compute_jtj / compute_jtr, algorithms.py:
+// 812-887): not on the solve path, which never writes J.  Elementwise kernels plus a
+// two-stage fixed-order fp64 reduction.
+
+// unit-normalised 3x3 Sobel with replicate padding (feature_gradient, 1844-1865):
+// f [P planes of H x W] -> g [P][2][H][W]
+__global__ __launch_bounds__(kThreads) void feature_gradient_kernel(const float* __restrict__ f, float* g, long P,
+                                                                    int H, int W) {
+  const long i = (long)blockIdx.x * kThreads + threadIdx.x;
+  const long HW = (long)H * W;
+  if (i >= P * HW) return;
+  const long pl = i / HW;
+  const int rem = (int)(i - pl * HW), y = rem / W, x = rem - y * W;
+  const float* F = f + pl * HW;
+  const int ym = max(y - 1, 0), yp = min(y + 1, H - 1), xm = max(x - 1, 0), xp = min(x + 1, W - 1);
+  auto at = [&](int yy, int xx) { return F[(long)yy * W + xx]; };
+  const float dx = ((at(ym, xp) - at(ym, xm)) + 2.0f * (at(y, xp) - at(y, xm))) + (at(yp, xp) - at(yp, xm));
+  const float dy = ((at(yp, xm) - at(ym, xm)) + 2.0f * (at(yp, x) - at(ym, x))) + (at(yp, xp) - at(ym, xp));
+  const float mag = sqrtf(dx * dx + dy * dy + 1e-8f);
+  g[pl * 2 * HW + rem] = dx / mag;
+  g[(pl * 2 + 1) * HW + rem] = dy / mag;
+}
+
+// compute_jacobian_warping (1884-1917) at the origin: Jx, Jy [B][HW][6]
+__global__ __launch_bounds__(kThreads) void warp_jacobian_kernel(const float* __restrict__ invD0,
+                                                                 const float* __restrict__ K,
+                                                                 const float* __restrict__ px,
+                                                                 const float* __restrict__ py, float* Jx, float* Jy,
+                                                                 int B, long HW) {
+  const long i = (long)blockIdx.x * kThreads + threadIdx.x;
+  if (i >= (long)B * HW) return;
+  const int b = (int)(i / HW);
+  const float x = px[i], y = py[i], d = invD0[i], fx = K[4 * b], fy = K[4 * b + 1], xy = x * y;
+  const float jx[6] = {-xy, 1.0f + x * x, -y, d, 0.0f, -d * x};
+  const float jy[6] = {-1.0f - y * y, xy, x, 0.0f, d, -d * y};
+  for (int k = 0; k < 6; ++k) {
+    Jx[6 * i + k] = jx[k] * fx;
+    Jy[6 * i + k] = jy[k] * fy;
+  }
+}
+
+// compose_inverse_jacobians (867-887) + compute_jacobian_dIdp (1867-1882):
+// a = -gx / s - r (s0 hx / s^3), b likewise, J = -(a Jx + b Jy) -> J [B][C][HW][6].
+// sigma0 / grad_sigma0 carry Cs = 1 or C channels.
+__global__ __launch_bounds__(kThreads) void inverse_jacobian_kernel(
+    const float* __restrict__ res, const float* __restrict__ sigma, const float* __restrict__ s0,
+    const float* __restrict__ gf0, const float* __restrict__ gs0, const float* __restrict__ Jx,
+    const float* __restrict__ Jy, float* J, int B, int C, int Cs, long HW) {
+  const long i = (long)blockIdx.x * kThreads + threadIdx.x;
+  if (i >= (long)B * C * HW) return;
+  const long bc = i / HW, p = i - bc * HW;
+  const int b = (int)(bc / C), c = (int)(bc - (long)b * C), cs = Cs == 1 ? 0 : c;
+  const long bs = (long)b * Cs + cs;
+  const float r = res[i], s = sigma[i], sz = s0[bs * HW + p];
+  const float s3 = (s * s) * s;
+  const float a = -gf0[(bc * 2) * HW + p] / s - r * ((sz * gs0[(bs * 2) * HW + p]) / s3);
+  const float bb = -gf0[(bc * 2 + 1) * HW + p] / s - r * ((sz * gs0[(bs * 2 + 1) * HW + p]) / s3);
+  const float* jx = Jx + ((long)b * HW + p) * 6;
+  const float* jy = Jy + ((long)b * HW + p) * 6;
+  for (int k = 0; k < 6; ++k) J[6 * i + k] = -(a * jx[k] + bb * jy[k]);
+}
+
+// J^T J, J^T r over n rows of 6 per pair: stage 1, block k of pair b sums rows
+// [n k / nb, n (k+1) / nb) into 27 fp64 partials (fixed order: thread-strided, then a
+// fixed tree); stage 2 sums a pair's nb partials in order.
+constexpr int kJtjBlocks = 128;
+__global__ __launch_bounds__(kThreads) void jtj_partial_kernel(const float* __restrict__ J,
+                                                               const float* __restrict__ r, long n, double* part) {
+  const int b = blockIdx.y, k = blockIdx.x, nb = gridDim.x;
+  const long beg = n * k / nb, end = n * (k + 1) / nb;
+  double acc[27];
+#pragma unroll
+  for (int q = 0; q < 27; ++q) acc[q] = 0.0;
+  const float* Jb = J + (size_t)b * n * 6;
+  const float* rb = r ? r + (size_t)b * n : nullptr;
+  for (long row = beg + threadIdx.x; row < end; row += kThreads) {
+    double j[6];
+#pragma unroll
+    for (int q = 0; q < 6; ++q) j[q] = Jb[6 * row + q];
+    int m = 0;
+#pragma unroll
+    for (int u = 0; u < 6; ++u)
+#pragma unroll
+      for (int v = u; v < 6; ++v) acc[m++] += j[u] * j[v];
+    if (rb) {
+      const double rr = rb[row];
+#pragma unroll
+      for (int u = 0; u < 6; ++u) acc[21 + u] += j[u] * rr;
+    }
+  }
+  __shared__ double sm[kThreads];
+#pragma unroll
+  for (int q = 0; q < 27; ++q) {
+    sm[threadIdx.x] = acc[q];
+    __syncthreads();
+    for (int w = kThreads / 2; w > 0; w >>= 1) {
+      if ((int)threadIdx.x < w) sm[threadIdx.x] += sm[threadIdx.x + w];
+      __syncthreads();
+    }
+    if (threadIdx.x == 0) part[((size_t)b * nb + k) * 27 + q] = sm[0];
+    __syncthreads();
+  }
+}
+
+__global__ __launch_bounds__(64) void jtj_final_kernel(const double* __restrict__ part, int nb, float* jtj,
+                                                       float* jtr) {
+  const int b = blockIdx.x, q = threadIdx.x;
+  if (q >= 27) return;
+  double s = 0.0;
+  for (int k = 0; k < nb; ++k) s += part[((size_t)b * nb + k) * 27 + q];
+  if (q < 21) {
+    int u = 0, m = q;
+    while (m >= 6 - u) {
+      m -= 6 - u;
+      ++u;
+    }
+    const int v = u + m;
+    jtj[36 * b + 6 * u + v] = (float)s;
+    jtj[36 * b + 6 * v + u] = (float)s;
+  } else if (jtr) {
+    jtr[6 * b + q - 21] = (float)s;
+  }
+}
+
 // One thread per (sample s, pair b): H = JtJ_b + diag(diag_add[s, b]) + 1e-6 tr(JtJ_b) I,
 // xi = H^-1 JtR_b (fp64 Cholesky), pose_out[s, b] = the inverse-compositional update of
 // pose_b (dpft_ic_damped_update).
@@ -3331,6 +3457,57 @@ __global__ __launch_bounds__(kThreads) void read_probe_kernel(const f32x4* __res
 }  // namespace
 
 extern "C" {
+
+int dpft_feature_gradient(const float* f, float* grad, int32_t B, int32_t C, int32_t H, int32_t W,
+                          void* hip_stream) {
+  if (!f || !grad || f == grad) return fail(DPFT_E_INVALID, "null or aliased pointer");
+  if (B < 1 || C < 1 || H < 1 || W < 1) return fail(DPFT_E_INVALID, "bad shape B=%d C=%d H=%d W=%d", B, C, H, W);
+  const long n = (long)B * C * H * W;
+  hipLaunchKernelGGL(feature_gradient_kernel, dim3((unsigned)((n + kThreads - 1) / kThreads)), dim3(kThreads), 0,
+                     static_cast<hipStream_t>(hip_stream), f, grad, (long)B * C, H, W);
+  return hip_check("feature_gradient_kernel");
+}
+
+int dpft_warp_jacobian(const float* invD0, const float* K, const float* px, const float* py, float* Jx, float* Jy,
+                       int32_t B, int32_t H, int32_t W, void* hip_stream) {
+  if (!invD0 || !K || !px || !py || !Jx || !Jy) return fail(DPFT_E_INVALID, "null pointer");
+  if (B < 1 || H < 1 || W < 1) return fail(DPFT_E_INVALID, "bad shape B=%d H=%d W=%d", B, H, W);
+  const long n = (long)B * H * W;
+  hipLaunchKernelGGL(warp_jacobian_kernel, dim3((unsigned)((n + kThreads - 1) / kThreads)), dim3(kThreads), 0,
+                     static_cast<hipStream_t>(hip_stream), invD0, K, px, py, Jx, Jy, B, (long)H * W);
+  return hip_check("warp_jacobian_kernel");
+}
+
+int dpft_inverse_jacobian(const float* res, const float* sigma, const float* sigma0, const float* grad_f0,
+                          const float* grad_sigma0, const float* Jx, const float* Jy, float* J, int32_t B, int32_t C,
+                          int32_t Cs, int32_t H, int32_t W, void* hip_stream) {
+  if (!res || !sigma || !sigma0 || !grad_f0 || !grad_sigma0 || !Jx || !Jy || !J)
+    return fail(DPFT_E_INVALID, "null pointer");
+  if (B < 1 || C < 1 || H < 1 || W < 1 || (Cs != 1 && Cs != C))
+    return fail(DPFT_E_INVALID, "bad shape B=%d C=%d Cs=%d H=%d W=%d", B, C, Cs, H, W);
+  const long n = (long)B * C * H * W;
+  hipLaunchKernelGGL(inverse_jacobian_kernel, dim3((unsigned)((n + kThreads - 1) / kThreads)), dim3(kThreads), 0,
+                     static_cast<hipStream_t>(hip_stream), res, sigma, sigma0, grad_f0, grad_sigma0, Jx, Jy, J, B, C,
+                     Cs, (long)H * W);
+  return hip_check("inverse_jacobian_kernel");
+}
+
+size_t dpft_normal_equations_workspace_size(int32_t B) { return (size_t)std::max(B, 0) * kJtjBlocks * 27 * sizeof(double); }
+
+int dpft_normal_equations(const float* J, const float* r, int64_t n, int32_t B, float* jtj, float* jtr, void* ws,
+                          size_t ws_bytes, void* hip_stream) {
+  if (!J || !jtj || !ws) return fail(DPFT_E_INVALID, "null pointer");
+  if (B < 1 || n < 1) return fail(DPFT_E_INVALID, "bad shape B=%d n=%lld", B, (long long)n);
+  if (ws_bytes < dpft_normal_equations_workspace_size(B))
+    return fail(DPFT_E_WORKSPACE, "workspace %zu < %zu", ws_bytes, dpft_normal_equations_workspace_size(B));
+  hipStream_t st = static_cast<hipStream_t>(hip_stream);
+  double* part = static_cast<double*>(ws);
+  hipLaunchKernelGGL(jtj_partial_kernel, dim3(kJtjBlocks, B), dim3(kThreads), 0, st, J, r, (long)n, part);
+  int rc = hip_check("jtj_partial_kernel");
+  if (rc) return rc;
+  hipLaunchKernelGGL(jtj_final_kernel, dim3(B), dim3(64), 0, st, part, kJtjBlocks, jtj, r ? jtr : nullptr);
+  return hip_check("jtj_final_kernel");
+}
 
 int dpft_ic_damped_update(const float* jtj, const float* jtr, const float* diag_add, int32_t S, int32_t B,
                           const float* R, const float* t, float* R_out, float* t_out, void* hip_stream) {

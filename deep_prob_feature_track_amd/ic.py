@@ -240,6 +240,77 @@ def iterate_poses(R, t, x0, x1, invD0, invD1, K, sigma0, sigma1, **kw):
     return jtj, jtr
 
 
+# ------------------------------------------------------------------ Jacobian API (materialised)
+def _dev_f32(name, t):
+    if not t.is_cuda:
+        raise RuntimeError(f"{name}: the HIP kernels need device tensors (got CPU); there is no CPU fallback")
+    if t.dtype != torch.float32:
+        raise TypeError(f"{name} must be float32 (got {t.dtype})")
+    return t.contiguous()
+
+
+def feature_gradient(f):
+    """Unit-normalised Sobel (feature_gradient, algorithms.py:1844-1865): f [B,C,H,W] ->
+    [B,C,2,H,W], (x, y) stacked on dim 2 as precompute_jacobian_components stacks them."""
+    f = _dev_f32("f", f)
+    B, C, H, W = f.shape
+    g = torch.empty(B, C, 2, H, W, dtype=torch.float32, device=f.device)
+    N.check(N.lib().dpft_feature_gradient(_ptr(f), _ptr(g), B, C, H, W, _stream(f.device)), "dpft_feature_gradient")
+    return g
+
+
+def warp_jacobian(invD0, K, px, py):
+    """compute_jacobian_warping at the origin (algorithms.py:1884-1917) -> Jx, Jy [B,HW,6]."""
+    invD0 = _dev_f32("invD0", invD0)
+    B, _, H, W = invD0.shape
+    K = _dev_f32("K", K.reshape(B, 4))
+    px = _dev_f32("px", px.expand(B, 1, H, W))
+    py = _dev_f32("py", py.expand(B, 1, H, W))
+    Jx = torch.empty(B, H * W, 6, dtype=torch.float32, device=invD0.device)
+    Jy = torch.empty_like(Jx)
+    N.check(N.lib().dpft_warp_jacobian(_ptr(invD0), _ptr(K), _ptr(px), _ptr(py), _ptr(Jx), _ptr(Jy), B, H, W,
+                                       _stream(invD0.device)), "dpft_warp_jacobian")
+    return Jx, Jy
+
+
+def inverse_jacobian(res, sigma, sigma0, grad_f0, grad_sigma0, Jx, Jy):
+    """compose_inverse_jacobians' J (algorithms.py:867-887): [B,C,HW,6], not masked.
+    sigma0 / grad_sigma0 may carry one channel or C (a channel broadcast is read once)."""
+    B, C, H, W = res.shape
+    res, sigma = _dev_f32("res", res), _dev_f32("sigma", sigma.expand(B, C, H, W))
+    s0, gs0 = sigma0, grad_sigma0
+    if s0.shape[1] != 1 and s0.stride(1) == 0:
+        s0, gs0 = s0[:, :1], gs0[:, :1]
+    Cs = s0.shape[1]
+    s0, gs0 = _dev_f32("sigma0", s0), _dev_f32("grad_sigma0", gs0)
+    gf0 = _dev_f32("grad_f0", grad_f0)
+    Jx, Jy = _dev_f32("Jx", Jx), _dev_f32("Jy", Jy)
+    J = torch.empty(B, C, H * W, 6, dtype=torch.float32, device=res.device)
+    N.check(N.lib().dpft_inverse_jacobian(_ptr(res), _ptr(sigma), _ptr(s0), _ptr(gf0), _ptr(gs0), _ptr(Jx), _ptr(Jy),
+                                          _ptr(J), B, C, Cs, H, W, _stream(res.device)), "dpft_inverse_jacobian")
+    return J
+
+
+def normal_equations(J, r=None):
+    """compute_jtj / compute_jtr (algorithms.py:812-834): J [B,...,6] (rows = every
+    channel and pixel), r [B,...] -> (JtJ [B,6,6], JtR [B,6,1] or None); fixed-order fp64."""
+    J = _dev_f32("J", J)
+    B = J.shape[0]
+    n = J.numel() // (6 * B)
+    if r is not None:
+        r = _dev_f32("r", r)
+        if r.numel() != B * n:
+            raise ValueError(f"r has {r.numel()} values, J has {B * n} rows")
+    L = N.lib()
+    nbytes = L.dpft_normal_equations_workspace_size(B)
+    ws = torch.empty(nbytes, dtype=torch.uint8, device=J.device)
+    jtj = torch.empty(B, 6, 6, dtype=torch.float32, device=J.device)
+    jtr = torch.empty(B, 6, 1, dtype=torch.float32, device=J.device) if r is not None else None
+    N.check(L.dpft_normal_equations(_ptr(J), _ptr(r), n, B, _ptr(jtj), _ptr(jtr), _ptr(ws), nbytes,
+                                    _stream(J.device)), "dpft_normal_equations")
+    return jtj, jtr
+
+
 def damped_update(JtJ, JtR, diag_add, pose):
     """S damped inverse-compositional updates per pair in one launch (dpft_ic_damped_update):
     JtJ [B,6,6], JtR [B,6], diag_add [S,B,6] or None (S = 1), pose ([B,3,3], [B,3(,1)])

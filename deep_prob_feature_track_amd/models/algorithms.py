@@ -509,6 +509,39 @@ class TrustRegionInverseWUncertainty(nn.Module):
             weights = torch.ones((1, 1, 1, 1), dtype=x0.dtype, device=x0.device).expand(B, C, H, W)
         return (pose, weights, out[2]) if self.uncer_prop else (pose, weights)
 
+    # ---- the reference solver's Jacobian API (algorithms.py:812-887), materialised by HIP
+    # kernels for callers that inspect J; forward never builds J (it stays in registers)
+    def precompute_jacobian_components(self, invD0, f0, sigma0, px, py, K, grad_interp=False, crd0=None):
+        """(grad_f0 [B,C,2,H,W], grad_sigma0, Jx_p [B,HW,6], Jy_p) -- algorithms.py:848-865."""
+        if grad_interp:
+            raise NotImplementedError("bilinear-interpolation gradients (grad_interp) belong to the forward "
+                                      "direction; the inverse path linearises at the origin")
+        grad_f0 = ic.feature_gradient(f0)
+        if sigma0.shape[1] != 1 and sigma0.stride(1) == 0:  # channel broadcast: one plane's gradient
+            grad_sigma0 = ic.feature_gradient(sigma0[:, :1]).expand(-1, sigma0.shape[1], -1, -1, -1)
+        else:
+            grad_sigma0 = ic.feature_gradient(sigma0)
+        Jx_p, Jy_p = ic.warp_jacobian(invD0, K, px, py)
+        return grad_f0, grad_sigma0, Jx_p, Jy_p
+
+    def compose_inverse_jacobians(self, res, sigma, sigma0, grad_f0, grad_sigma0, Jx_p, Jy_p):
+        """(J [B,C,HW,6], J_res_trs [B,C,3,H,W], J_res_rot) -- algorithms.py:867-887; the
+        two parts are of -J, the chained derivative before the reference's sign flip."""
+        B, C, H, W = sigma0.shape
+        J = ic.inverse_jacobian(res, sigma, sigma0, grad_f0, grad_sigma0, Jx_p, Jy_p)
+        J_res_rot, J_res_trs = (-J).view(B, C, H, W, 6).split(3, dim=-1)
+        if not torch.isfinite(J).all():
+            raise AssertionError("non-finite Jacobian (reference: assert check_nan(J_res_p) == 0)")
+        return J, J_res_trs.permute(0, 1, 4, 2, 3), J_res_rot.permute(0, 1, 4, 2, 3)
+
+    def compute_jtj(self, jac):
+        """J [B,C,HW,6] -> JtJ [B,6,6] (algorithms.py:812-820)."""
+        return ic.normal_equations(jac)[0]
+
+    def compute_jtr(self, jac, res):
+        """J [B,C,HW,6], res [B,C,H,W] -> JtR [B,6,1] (algorithms.py:822-834)."""
+        return ic.normal_equations(jac, res)[1]
+
     def forward_residuals(self, pose10, x0, x1, invD0, invD1, K, sigma0, sigma1, wPrior=None,
                           depth0=None, depth1=None, vis_res=True, obj_mask0=None, obj_mask1=None):
         assert sigma0 is not None and sigma1 is not None

@@ -250,6 +250,33 @@ int dpft_preprocess_depth(const float* depth, int32_t B, int32_t H, int32_t W, i
 int dpft_pack_features(const float* src, float* dst, int32_t B, int32_t C, int32_t H, int32_t W, void* hip_stream);
 
 /*
+ * Jacobian API, materialised -- the reference solver's methods that the fused solve
+ * never needs (it keeps J in registers); kept for callers and tests that inspect J.
+ *  dpft_feature_gradient    feature_gradient (algorithms.py:1844-1865): unit-normalised
+ *                           replicate-padded Sobel, f [B,C,H,W] -> grad [B,C,2,H,W].
+ *  dpft_warp_jacobian       compute_jacobian_warping (1884-1917) at the origin:
+ *                           invD0, px, py [B,1,H,W], K [B,4] -> Jx, Jy [B,HW,6].
+ *  dpft_inverse_jacobian    compose_inverse_jacobians (867-887) + compute_jacobian_dIdp
+ *                           (1867-1882): res, sigma [B,C,H,W], sigma0 [B,Cs,H,W],
+ *                           grad_f0 [B,C,2,H,W], grad_sigma0 [B,Cs,2,H,W] (Cs = 1 or C)
+ *                           -> J [B,C,HW,6] (not masked, as the reference).
+ *  dpft_normal_equations    compute_jtj / compute_jtr (812-834): J [B,n,6], r [B,n]
+ *                           (NULL: JtJ only) -> jtj [B,6,6], jtr [B,6]; fp64 partials in
+ *                           a fixed order (deterministic); workspace of
+ *                           dpft_normal_equations_workspace_size(B) bytes.
+ */
+int dpft_feature_gradient(const float* f, float* grad, int32_t B, int32_t C, int32_t H, int32_t W,
+                          void* hip_stream);
+int dpft_warp_jacobian(const float* invD0, const float* K, const float* px, const float* py, float* Jx, float* Jy,
+                       int32_t B, int32_t H, int32_t W, void* hip_stream);
+int dpft_inverse_jacobian(const float* res, const float* sigma, const float* sigma0, const float* grad_f0,
+                          const float* grad_sigma0, const float* Jx, const float* Jy, float* J, int32_t B, int32_t C,
+                          int32_t Cs, int32_t H, int32_t W, void* hip_stream);
+size_t dpft_normal_equations_workspace_size(int32_t B);
+int dpft_normal_equations(const float* J, const float* r, int64_t n, int32_t B, float* jtj, float* jtr, void* ws,
+                          size_t ws_bytes, void* hip_stream);
+
+/*
  * Damped inverse-compositional update of 'Direct-ResVol' (DirectSolverNet,
  * algorithms.py:1644-1691, then inverse_update_pose 2017-2054), for S damping choices
  * per pair at once: H[s,b] = JtJ[b] + diag(diag_add[s,b]) + 1e-6 tr(JtJ[b]) I,

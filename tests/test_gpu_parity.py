@@ -378,3 +378,69 @@ def test_iterate_poses_equals_per_pose_iterate():
         _, _, jtj1, jtr1, _ = ic.iterate((Rs[s], ts[s].view(B, 3, 1)), lv["f0"], lv["f1"], lv["invD0"], lv["invD1"], K,
                                          None, None, first=False, update=False, **kw)
         assert torch.equal(jtj[s], jtj1) and torch.equal(jtr[s], jtr1)
+
+
+def test_jacobian_api_matches_oracle_and_fused_kernel():
+    """The reference solver's Jacobian API on the module (precompute_jacobian_components,
+    compose_inverse_jacobians, compute_jtj, compute_jtr; algorithms.py:812-887),
+    materialised by HIP kernels, against the oracle's restatement of each step at the
+    golden case's initial pose, and its J^T J / J^T r against the fused kernel's."""
+    from oracle import ic_oracle as O
+    from deep_prob_feature_track_amd import ic
+    from deep_prob_feature_track_amd.models.algorithms import TrustRegionInverseWUncertainty
+    dev = _dev()
+    case, z = golden_io.load("cfg1_160x120_c8")
+    lv = golden_io.levels_torch(case, torch.float32, "cpu")[0]
+    R0, t0 = golden_io.init_pose(case, torch.float32, "cpu")
+    K = torch.from_numpy(case["K"])
+    B, C, H, W = lv["f0"].shape
+    x, y = O.pixel_rays(B, H, W, K)
+    s0C, s1C = lv["s0"].expand(B, C, H, W), lv["s1"].expand(B, C, H, W)
+    # the oracle in fp64 on the same (fp32-valued) inputs: the normal equations sum ~1e6
+    # products, where an fp32 bmm drifts by a few 1e-5 of its result
+    dd = lambda a: a.double()
+    rw, r, sigma, invalid = O.residuals(dd(R0), dd(t0), dd(lv["invD0"]), dd(lv["invD1"]), dd(lv["f0"]), dd(lv["f1"]),
+                                        dd(s0C), dd(s1C), dd(x), dd(y), dd(K))
+    gx, gy = O.sobel(dd(lv["f0"]))
+    hx, hy = O.sobel(dd(s0C))
+    Jx, Jy = O.warp_jacobian(dd(lv["invD0"]), dd(K), dd(x), dd(y))
+    J_ref = O.inverse_jacobian(r, sigma, dd(s0C), (gx, gy), (hx, hy), Jx, Jy)
+    JtJ_ref, JtR_ref = O.normal_equations(J_ref, rw)
+    gx, gy, hx, hy, Jx, Jy, J_ref = (a.float() for a in (gx, gy, hx, hy, Jx, Jy, J_ref))
+    r, sigma, rw, JtJ_ref, JtR_ref = (a.float() for a in (r, sigma, rw, JtJ_ref, JtR_ref))
+
+    tr = TrustRegionInverseWUncertainty()
+    g = lambda a: a.to(dev)
+    gf0, gs0, Jxh, Jyh = tr.precompute_jacobian_components(g(lv["invD0"]), g(lv["f0"]), g(s0C), g(x), g(y), g(K))
+    assert gf0.shape == (B, C, 2, H, W) and gs0.shape == (B, C, 2, H, W) and Jxh.shape == (B, H * W, 6)
+    # unit-normalised gradients: where the raw Sobel of a flat patch is rounding noise
+    # (|dx|, |dy| ~ 1e-7, normalised by sqrt(1e-8)) its value depends on the summation
+    # order (conv2d's vs this kernel's): one ulp of sigma ~ 1 (1.2e-7) becomes 1.2e-3
+    torch.testing.assert_close(gf0.cpu(), torch.stack((gx, gy), 2), rtol=0, atol=5e-4)
+    torch.testing.assert_close(gs0.cpu(), torch.stack((hx, hy), 2), rtol=0, atol=3e-3)
+    torch.testing.assert_close(Jxh.cpu(), Jx, rtol=1e-6, atol=1e-4)
+    torch.testing.assert_close(Jyh.cpu(), Jy, rtol=1e-6, atol=1e-4)
+    J, J_trs, J_rot = tr.compose_inverse_jacobians(g(r), g(sigma), g(s0C), gf0, gs0, Jxh, Jyh)
+    assert J.shape == (B, C, H * W, 6) and J_trs.shape == (B, C, 3, H, W) and J_rot.shape == (B, C, 3, H, W)
+    # J inherits the gradient's order-dependent noise at flat patches (bounded by
+    # 1.2e-3 |Jx| / sigma on the unit-gradient scale): every element within 2e-3 of max|J|,
+    # and all but <= 0.05 % of them within 1e-5 of it
+    Jmax = J_ref.abs().max().item()
+    d = (J.cpu() - J_ref).abs()
+    assert d.max().item() <= 2e-3 * Jmax
+    assert (d > 1e-5 * Jmax).float().mean().item() <= 5e-4
+    d_rot = (J_rot.cpu() - (-J_ref).view(B, C, H, W, 6)[..., :3].permute(0, 1, 4, 2, 3)).abs()
+    assert d_rot.max().item() <= 2e-3 * Jmax
+    JtJ = tr.compute_jtj(J)
+    JtR = tr.compute_jtr(J, g(rw))
+    torch.testing.assert_close(JtJ.cpu(), JtJ_ref, rtol=1e-5, atol=1e-6 * JtJ_ref.abs().max().item())
+    torch.testing.assert_close(JtR.cpu(), JtR_ref, rtol=1e-4, atol=1e-5 * JtR_ref.abs().max().item())
+    # the fused kernel's normal equations at the same pose (never materialising J); its
+    # invalid set is the fp32 one (bit-exact vs the reference's CPU arithmetic), so J^T r
+    # is compared with the fp32 oracle residual (an fp64 warp flips a few boundary pixels)
+    rw32 = O.residuals(R0, t0, lv["invD0"], lv["invD1"], lv["f0"], lv["f1"], s0C, s1C, x, y, K)[0]
+    JtR = tr.compute_jtr(J, g(rw32))
+    _, _, JtJ_f, JtR_f, _ = ic.iterate((g(R0), g(t0)), g(lv["f0"]), g(lv["f1"]), g(lv["invD0"]), g(lv["invD1"]), g(K),
+                                       g(lv["s0"]), g(lv["s1"]), first=True, update=False)
+    torch.testing.assert_close(JtJ_f.cpu(), JtJ.cpu(), rtol=1e-5, atol=1e-6 * JtJ_ref.abs().max().item())
+    torch.testing.assert_close(JtR_f.cpu(), JtR.cpu().view(B, 6), rtol=1e-4, atol=1e-5 * JtR_ref.abs().max().item())
