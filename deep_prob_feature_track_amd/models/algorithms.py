@@ -407,6 +407,27 @@ class TrustRegionBase(nn.Module):
     def _learned_weights(self):
         return self.mEstimator is not None and getattr(self.mEstimator, 'D', -1) > 0
 
+    def precompute_Jacobian(self, invD, x, px, py, K):
+        """Template image Jacobian J = gx Jx + gy Jy per channel and pixel (algorithms.py:
+        103-121) -> [B, C*HW, 6], materialised by the HIP inverse-Jacobian kernel with sigma
+        = 1 and a zero residual (its a = -gx / sigma, J = -(a Jx + b Jy)).  The fused
+        iteration never builds it."""
+        B, C, H, W = x.shape
+        g = ic.feature_gradient(x)
+        Jx_p, Jy_p = ic.warp_jacobian(invD, K, px, py)
+        one = torch.ones((1, 1, 1, 1), dtype=torch.float32, device=x.device).expand(B, C, H, W)
+        zero = torch.zeros((1, 1, 1, 1), dtype=torch.float32, device=x.device)
+        J = ic.inverse_jacobian(zero.expand(B, C, H, W), one, one[:, :1].expand(B, C, H, W),
+                                g, zero.expand(B, 1, 2, H, W), Jx_p, Jy_p)
+        return J.view(B, C * H * W, 6)
+
+    def GN_solver(self, JtJ, JtR, pose0):
+        """lev_mar_H + inverse_update_pose (algorithms.py:105-107, 2094-2103, 2017-2054) in
+        one launch (dpft_ic_damped_update)."""
+        B = JtJ.shape[0]
+        R, t = ic.damped_update(JtJ, JtR.reshape(B, 6), None, pose0)
+        return [R[0], t[0]]
+
     def _weights(self, pose, x0, x1, invD0, invD1, K, wPrior, obj_mask0, obj_mask1):
         """(weights [B,1,H,W] of the learned estimator, residual map, occlusion) or Nones."""
         if not self._learned_weights():
@@ -533,6 +554,16 @@ class TrustRegionInverseWUncertainty(nn.Module):
         if not torch.isfinite(J).all():
             raise AssertionError("non-finite Jacobian (reference: assert check_nan(J_res_p) == 0)")
         return J, J_res_trs.permute(0, 1, 4, 2, 3), J_res_rot.permute(0, 1, 4, 2, 3)
+
+    def GN_solver(self, JtJ, JtR, pose0, direction='inverse'):
+        """lev_mar_H + inverse_update_pose (algorithms.py:836-846, 2094-2103, 2017-2054):
+        H = JtJ + 1e-6 tr(JtJ) I solved in fp64 and the inverse-compositional update, in
+        one launch (dpft_ic_damped_update)."""
+        if direction != 'inverse':
+            raise NotImplementedError("the forward-compositional update belongs to the U_FC tracker")
+        B = JtJ.shape[0]
+        R, t = ic.damped_update(JtJ, JtR.reshape(B, 6), None, pose0)
+        return [R[0], t[0]]
 
     def compute_jtj(self, jac):
         """J [B,C,HW,6] -> JtJ [B,6,6] (algorithms.py:812-820)."""

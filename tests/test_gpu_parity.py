@@ -444,3 +444,34 @@ def test_jacobian_api_matches_oracle_and_fused_kernel():
                                        g(lv["s0"]), g(lv["s1"]), first=True, update=False)
     torch.testing.assert_close(JtJ_f.cpu(), JtJ.cpu(), rtol=1e-5, atol=1e-6 * JtJ_ref.abs().max().item())
     torch.testing.assert_close(JtR_f.cpu(), JtR.cpu().view(B, 6), rtol=1e-4, atol=1e-5 * JtR_ref.abs().max().item())
+
+
+def test_gn_solver_and_ic_precompute_jacobian_match_oracle():
+    """GN_solver (lev_mar_H + inverse_update_pose) of both solver modules and the IC
+    tracker's precompute_Jacobian (algorithms.py:103-121, 836-846) against the fp64 oracle."""
+    from oracle import ic_oracle as O
+    from deep_prob_feature_track_amd.models.algorithms import TrustRegionBase, TrustRegionInverseWUncertainty
+    dev = _dev()
+    case, z = golden_io.load("cfg1_160x120_c8")
+    lv = golden_io.levels_torch(case, torch.float32, "cpu")[0]
+    R0, t0 = golden_io.init_pose(case, torch.float32, "cpu")
+    K = torch.from_numpy(case["K"])
+    B, C, H, W = lv["f0"].shape
+    x, y = O.pixel_rays(B, H, W, K)
+    dd = lambda a: a.double()
+    J_ref = O.ic_jacobian(dd(lv["invD0"]), dd(lv["f0"]), dd(x), dd(y), dd(K)).float()
+    g = lambda a: a.to(dev)
+    J = TrustRegionBase().precompute_Jacobian(g(lv["invD0"]), g(lv["f0"]), g(x), g(y), g(K))
+    assert J.shape == (B, C * H * W, 6)
+    Jmax = J_ref.abs().max().item()
+    d = (J.cpu() - J_ref).abs()   # gradient noise at flat patches, as in the Jacobian API test
+    assert d.max().item() <= 2e-3 * Jmax and (d > 1e-5 * Jmax).float().mean().item() <= 5e-4
+    gen = torch.Generator().manual_seed(5)
+    A = torch.randn(B, 6, 30, generator=gen, dtype=torch.float64)
+    JtJ = A @ A.transpose(1, 2)
+    JtR = 0.01 * torch.randn(B, 6, 1, generator=gen, dtype=torch.float64)
+    R_ref, t_ref, _ = O.damped_solve_update(JtJ, JtR, dd(R0), dd(t0).view(B, 3, 1))
+    for mod in (TrustRegionInverseWUncertainty(), TrustRegionBase()):
+        R, t = mod.GN_solver(g(JtJ.float()), g(JtR.float()), [g(R0), g(t0)])
+        assert (R.cpu().double() - R_ref).abs().max().item() < 2e-6
+        assert (t.cpu().double().view(B, 3, 1) - t_ref).abs().max().item() < 2e-6
