@@ -24,7 +24,8 @@ KEYS = json.load(open(os.path.join(HERE, "model_keys.json")))
 def build(spec, mest=None, solver=None, no_weight_sharing=False):
     return LeastSquareTracking(spec["encoder"], spec["uncertainty"], 3, mest or spec.get("mest", "None"),
                                solver or spec.get("solver", "Direct-Nodamping"),
-                               options=default_options(**spec["opts"]), no_weight_sharing=no_weight_sharing)
+                               options=default_options(**spec["opts"]), no_weight_sharing=no_weight_sharing,
+                               **spec.get("ctor", {}))
 
 
 @pytest.mark.parametrize("name", sorted(G.KEY_VARIANTS))
