@@ -47,3 +47,58 @@ def gather_poses(R, t, out=None, async_op=False):
     else:
         work = dist.all_gather(list(out.chunk(world, 0)), P, async_op=async_op)
     return (out, work) if async_op else out
+
+
+def pack_results(R, t, jtj=None, status=None):
+    """Per-pair result rows: [R(9), t(3)] + optionally JtJ(36) + a
+    non-finite flag(1) -> [B, 12 | 48 | 13 | 49] fp32.  `status` is the solve's status
+    word (one per batch): every pair row carries it."""
+    B = R.shape[0]
+    cols = [R.reshape(B, 9).to(torch.float32), t.reshape(B, 3).to(torch.float32)]
+    if jtj is not None:
+        cols.append(jtj.reshape(B, 36).to(torch.float32))
+    if status is not None:
+        cols.append(status.reshape(1, 1).to(torch.float32).expand(B, 1))
+    return torch.cat(cols, 1).contiguous()
+
+
+def unpack_results(P, with_jtj=False, with_status=False):
+    """Inverse of pack_results: dict(R [N,3,3], t [N,3,1][, jtj [N,6,6]][, status [N]])."""
+    out = dict(R=P[:, :9].reshape(-1, 3, 3), t=P[:, 9:12].reshape(-1, 3, 1))
+    c = 12
+    if with_jtj:
+        out["jtj"] = P[:, c:c + 36].reshape(-1, 6, 6)
+        c += 36
+    if with_status:
+        out["status"] = P[:, c].to(torch.int32)
+    return out
+
+
+def gather_results(R, t, jtj=None, status=None, n_pairs=None):
+    """All-gather every rank's result rows into [n_pairs, F] in pair order, for shards
+    of unequal size too (n_pairs not a multiple of the world size: shard_range's
+    split).  Each rank pads its rows to ceil(n_pairs / world) for the single
+    fixed-size collective and the padding is dropped after it.  n_pairs None: equal
+    shards (world * B rows)."""
+    P = pack_results(R, t, jtj, status)
+    world, rank = dist.get_world_size(), dist.get_rank()
+    B, F = P.shape
+    if n_pairs is None:
+        n_pairs = world * B
+    b, e = shard_range(n_pairs, world, rank)
+    if e - b != B:
+        raise ValueError(f"rank {rank} holds {B} pairs, its shard of {n_pairs} is {e - b}")
+    cap = -(-n_pairs // world)
+    if B < cap:
+        P = torch.cat((P, P.new_zeros(cap - B, F)), 0)
+    full = torch.empty(world * cap, F, dtype=P.dtype, device=P.device)
+    if dist.get_backend() == "nccl":
+        dist.all_gather_into_tensor(full, P)
+    else:
+        dist.all_gather(list(full.chunk(world, 0)), P)
+    rows = []
+    for r in range(world):
+        rb, re_ = shard_range(n_pairs, world, r)
+        rows.append(full[r * cap:r * cap + (re_ - rb)])
+    return torch.cat(rows, 0)
+

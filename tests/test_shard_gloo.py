@@ -99,3 +99,47 @@ def test_two_rank_gloo_gather_matches_per_shard_solves():
         expect.append(shard.pack_poses(*_solve_pairs(PAIRS[b:e])))
     assert torch.equal(gathered, torch.cat(expect, 0))
     assert torch.equal(gathered_async, gathered)
+
+
+def _worker_results(rank, world, port, q, n_pairs):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    torch.set_num_threads(1)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        b, e = shard.shard_range(n_pairs, world, rank)
+        idx = torch.arange(b, e, dtype=torch.float32).view(-1, 1, 1)
+        R = idx + 0.01 * torch.arange(9, dtype=torch.float32).view(1, 3, 3)
+        t = -idx.view(-1, 1, 1) * torch.ones(1, 3, 1)
+        jtj = idx * torch.ones(1, 6, 6) + torch.eye(6)
+        status = torch.tensor([rank], dtype=torch.int32)
+        out = shard.gather_results(R, t, jtj=jtj, status=status, n_pairs=n_pairs)
+        if rank == 0:
+            q.put(out.clone())
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("n_pairs", [4, 7])
+def test_two_rank_gather_results_ragged_shards(n_pairs):
+    """gather_results: poses + JtJ + status rows of unequal shards (7 pairs on 2 ranks:
+    4 + 3) come back in pair order, padding dropped (SURVEY.md 8e's gathered record)."""
+    world = 2
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker_results, args=(r, world, port, q, n_pairs)) for r in range(world)]
+    for p in procs:
+        p.start()
+    out = q.get(timeout=120)
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    res = shard.unpack_results(out, with_jtj=True, with_status=True)
+    assert out.shape == (n_pairs, 49)
+    idx = torch.arange(n_pairs, dtype=torch.float32)
+    assert torch.equal(res["R"][:, 0, 0], idx) and torch.equal(res["t"][:, 2, 0], -idx)
+    assert torch.equal(res["jtj"][:, 0, 1], idx)
+    spans = [shard.shard_range(n_pairs, world, r) for r in range(world)]
+    owner = torch.cat([torch.full((e - b,), r, dtype=torch.int32) for r, (b, e) in enumerate(spans)])
+    assert torch.equal(res["status"], owner)
+
