@@ -186,11 +186,15 @@ def cpu_baseline(levels_gpu, K, R_gpu, t_gpu):
     dR = (R_gpu[:1].cpu() - Ro).abs().max().item()
     dt = (t_gpu[:1].cpu().view(1, 3) - to.view(1, 3)).abs().max().item()
     # 3D end-point error between the two poses over frame-0 points (criterions.py:101-136)
-    from deep_prob_feature_track_amd.metrics import epe3d_between
+    from deep_prob_feature_track_amd.metrics import epe3d_between, rpe
     d0 = 1.0 / lv[0]["invD0"].clamp(min=1e-6)
     epe = epe3d_between(R_gpu[:1].cpu(), t_gpu[:1].cpu().view(1, 3), Ro, to.view(1, 3), d0,
                         Kc, invalid=(lv[0]["invD0"] <= 0)).item()
-    return best, dR, dt, epe, one_thread
+    # translational relative pose error between the two estimates (criterions.py
+    # compute_RPE_loss; its angle term is floored at acos(1 - 1e-7) = 4.5e-4 rad by the
+    # reference's clamp, so the rotation is reported as max |dR| above)
+    _, trs = rpe(R_gpu[:1].cpu(), t_gpu[:1].cpu().view(1, 3), Ro, to.view(1, 3))
+    return best, dR, dt, epe, one_thread, trs.item()
 
 
 def main():
@@ -401,14 +405,14 @@ def main():
 
     cpu = None
     if rank == 0 and world == 1 and not a.no_cpu_baseline:
-        best, dR, dt, epe, one_thread = cpu_baseline(levels_nchw, K, R, t)
+        best, dR, dt, epe, one_thread, rpe_trs = cpu_baseline(levels_nchw, K, R, t)
         cpu = {"value": LEVELS * ITERS / best, "unit": "IC iterations/s",
                "cores": torch.get_num_threads(), "kind": "port", "cpu_model": cpu_model(),
                "value_1_thread": LEVELS * ITERS / one_thread, "seconds_per_pair_1_thread": one_thread,
                "sample": "1 pair, 640x480 C=32, 4 levels x 3 iters, oracle/ic_oracle.py (PyTorch-CPU fp32 "
                          "restatement of algorithms.py:611-723), best of 2 after 1 warm-up",
                "seconds_per_pair": best, "gpu_vs_oracle_max_abs_dR": dR, "gpu_vs_oracle_max_abs_dt": dt,
-               "gpu_vs_oracle_3dpe_m": epe}
+               "gpu_vs_oracle_3dpe_m": epe, "gpu_vs_oracle_rpe_trans_m": rpe_trs}
 
     if rank == 0:
         line = {
