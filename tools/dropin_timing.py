@@ -20,8 +20,8 @@ from deep_prob_feature_track_amd.models.LeastSquareTracking import LeastSquareTr
 ap = argparse.ArgumentParser()
 ap.add_argument("--reps", type=int, default=20)
 ap.add_argument("--batch", type=int, default=8)
-ap.add_argument("--config", default="uic", choices=["uic", "deepic"],
-                help="uic: ConvRGBD2 + laplacian U_IC tracker, C=32; deepic: RGB features, IC tracker, "
+ap.add_argument("--config", default="uic", choices=["uic", "uic8", "deepic"],
+                help="uic: ConvRGBD2 + laplacian U_IC tracker, C=32 (uic8: C=8); deepic: RGB features, IC tracker, "
                      "MultiScale2w M-estimator, Direct-ResVol")
 ap.add_argument("--down", type=int, default=1, help="image subsampling (1: 640x480)")
 a = ap.parse_args()
@@ -29,9 +29,10 @@ dev = torch.device("cuda:0")
 if os.environ.get("DPFT_DROPIN_BENCHMARK"):  # MIOpen algorithm search for the encoder convs
     torch.backends.cudnn.benchmark = True
 torch.manual_seed(0)
-if a.config == "uic":
+if a.config in ("uic", "uic8"):
     m = LeastSquareTracking("ConvRGBD2", "laplacian", 3, "None", "Direct-Nodamping",
-                            options=default_options(feature_channel=32, uncertainty_channel=1, feature_extract="conv",
+                            options=default_options(feature_channel=32 if a.config == "uic" else 8,
+                                                    uncertainty_channel=1, feature_extract="conv",
                                                     remove_tru_sigma=True)).to(dev).eval()
 else:
     m = LeastSquareTracking("RGB", "None", 3, "MultiScale2w", "Direct-ResVol",
