@@ -18,12 +18,19 @@ import torch
 from . import _native as N
 
 _ws_cache = {}
+_ws_retired = []
 
 
 def _workspace(device, nbytes):
-    key = (device.type, device.index)
+    """The per-(device, stream) workspace of the one-call entry points: one per stream
+    because concurrent launches must not share completion counters (dpft_ic.h).  A
+    buffer outgrown by a larger call is kept alive, not freed: a HIP graph captured
+    with it still replays into it."""
+    key = (device.type, device.index, torch.cuda.current_stream(device).cuda_stream)
     buf = _ws_cache.get(key)
     if buf is None or buf.numel() < nbytes:
+        if buf is not None:
+            _ws_retired.append(buf)
         # zero-filled once: the library's completion counters live in it (dpft_ic.h)
         buf = torch.zeros(max(nbytes, 1 << 20), dtype=torch.uint8, device=device)
         _ws_cache[key] = buf

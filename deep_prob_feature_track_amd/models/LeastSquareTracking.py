@@ -174,7 +174,11 @@ class LeastSquareTracking(nn.Module):
         finally:
             for l in (3, 2, 1, 0):
                 getattr(self, f'tr_update{l}')._deferred_status = None
-        if status is not None:
+        self.last_status = status
+        # under HIP-graph capture the host read is deferred to the caller (check
+        # `model.last_status` after a replay, e.g. ic.check_status): forward is then
+        # capturable whole -- encoder, pyramids and the four levels in one graph
+        if status is not None and not torch.cuda.is_current_stream_capturing():
             ic.check_status(status)
         return pose
 

@@ -14,10 +14,18 @@ _RGB_MEAN = (0.4914, 0.4822, 0.4465)
 _RGB_STD = (0.2023, 0.1994, 0.2010)
 
 
+_NORM_CONSTS = {}
+
+
 def color_normalize(color):
-    """Per-channel (x - mean) / std of an RGB batch [B,3,H,W] (submodules.py:20-23)."""
-    mean = torch.tensor(_RGB_MEAN, dtype=color.dtype, device=color.device).view(1, 3, 1, 1)
-    std = torch.tensor(_RGB_STD, dtype=color.dtype, device=color.device).view(1, 3, 1, 1)
+    """Per-channel (x - mean) / std of an RGB batch [B,3,H,W] (submodules.py:20-23).
+    The constants are copied to the device once per (device, dtype): a host-to-device
+    copy per call would also make forward impossible to capture in a HIP graph."""
+    key = (color.device, color.dtype)
+    if key not in _NORM_CONSTS:
+        _NORM_CONSTS[key] = (torch.tensor(_RGB_MEAN, dtype=color.dtype, device=color.device).view(1, 3, 1, 1),
+                             torch.tensor(_RGB_STD, dtype=color.dtype, device=color.device).view(1, 3, 1, 1))
+    mean, std = _NORM_CONSTS[key]
     return (color - mean) / std
 
 

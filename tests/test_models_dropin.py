@@ -166,3 +166,39 @@ def test_convergence_basin_driver_outputs():
     d2 = CB.evaluate_2d_convergence_basin(m, T["img0"], T["img1"], T["depth0"], T["depth1"], Rt, T["K"],
                                           pert_samples=3)
     np.testing.assert_allclose(d2["avg_loss"][0, 1, 1], z["res_pose_loss"], rtol=1e-3)
+
+
+@pytest.mark.gpu
+def test_forward_captured_in_a_hip_graph():
+    """The whole drop-in forward (encoder, pyramids, four solver levels) captured into one
+    HIP graph and replayed on new input contents equals eager forward calls; the
+    non-finite status word is left in `last_status` for the caller."""
+    from deep_prob_feature_track_amd import ic
+    m, T = _loaded("convrgbd2_c8", "cuda")
+    z = np.load(os.path.join(HERE, "model_convrgbd2_c8.npz"), allow_pickle=False)
+    static = {k: T[k].clone() for k in ("img0", "img1", "depth0", "depth1", "K")}
+    with torch.no_grad():
+        s = torch.cuda.Stream()
+        s.wait_stream(torch.cuda.current_stream())
+        with torch.cuda.stream(s):
+            m(**{k: static[k] for k in static})
+        torch.cuda.current_stream().wait_stream(s)
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g):
+            R_g, t_g = m(static["img0"], static["img1"], static["depth0"], static["depth1"], static["K"])
+        status = m.last_status
+        g.replay()
+        torch.cuda.synchronize()
+        ic.check_status(status)
+        assert np.abs(R_g.cpu().numpy() - z["R"]).max() < 1e-4
+        R_e, t_e = m(T["img0"], T["img1"], T["depth0"], T["depth1"], T["K"])
+        assert (R_g - R_e).abs().max().item() < 1e-5 and (t_g - t_e).abs().max().item() < 1e-5
+        # new contents in the static inputs: the replay tracks the swapped pairs
+        static["img0"].copy_(T["img1"])
+        static["img1"].copy_(T["img0"])
+        static["depth0"].copy_(T["depth1"])
+        static["depth1"].copy_(T["depth0"])
+        g.replay()
+        torch.cuda.synchronize()
+        R_s, t_s = m(T["img1"], T["img0"], T["depth1"], T["depth0"], T["K"])
+        assert (R_g - R_s).abs().max().item() < 1e-5 and (t_g - t_s).abs().max().item() < 1e-5

@@ -59,6 +59,18 @@ def timed(fn):
 
 
 full = timed(lambda: m.forward(img0, img1, d0, d1, K))
+if os.environ.get("DPFT_DROPIN_GRAPH"):  # the whole forward captured into one HIP graph
+    with torch.no_grad():
+        s = torch.cuda.Stream()
+        s.wait_stream(torch.cuda.current_stream())
+        with torch.cuda.stream(s):
+            m.forward(img0, img1, d0, d1, K)
+        torch.cuda.current_stream().wait_stream(s)
+        graph = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(graph):
+            m.forward(img0, img1, d0, d1, K)
+    gr = timed(graph.replay)
+    print(f"forward as one HIP graph replay: {gr:.2f} ms per call (eager {full:.2f} ms)", flush=True)
 pre = timed(lambda: m._preprocess(img0, img1, d0, d1))
 H, W = img0.shape[2:]
 print(f"drop-in forward ({a.config}) B={B} {W}x{H}: {full:.2f} ms per call; _preprocess {pre:.2f} ms; "
