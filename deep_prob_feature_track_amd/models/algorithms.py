@@ -258,7 +258,18 @@ class DirectSolverNet(nn.Module):
     def forward(self, *args, **kwargs):
         raise NotImplementedError("DirectSolverNet is driven by TrustRegionBase (resvol_step); not on the U_IC path")
 
-    def resvol_step(self, pose, level_args, weights, obj_mask0, obj_mask1, first):
+    def replicate(self, level_args, weights, obj_mask1):
+        """The level's inputs repeated `samples` times along the batch (trial s of pair b
+        at s * B + b), made once per level call: the ten residual-volume samples of every
+        iteration then run as ONE no-update launch over samples x pairs.  The IC tracker
+        has no batch-global term (no truncated sigma), so each (trial, pair) row is
+        solved exactly as alone."""
+        S = self.samples
+        x0, x1, invD0, invD1, K = level_args
+        rep = lambda a: None if a is None else a.repeat(S, *([1] * (a.dim() - 1)))  # noqa: E731
+        return rep(x0), rep(x1), rep(invD0), rep(invD1), rep(K), rep(weights), rep(obj_mask1)
+
+    def resvol_step(self, pose, level_args, weights, obj_mask0, obj_mask1, first, replicated=None):
         """One Gauss-Newton step with the learned residual-volume damping
         (__regularize_residual_volume, algorithms.py:1644-1691, then inverse_update_pose):
         JtWJ, JtWr at `pose` (obj_mask0 only on a level's first step, 72-73 / 77-78), ten
@@ -277,8 +288,15 @@ class DirectSolverNet(nn.Module):
         # the S trial poses (JtJ + lambda_s diag(JtJ) + 1e-6 tr I) in one launch, their
         # J^T W r through one LevelCall, the learned damping's update in one more launch
         R_s, t_s = ic.damped_update(JtJ, JtR, self._lambdas * torch.diagonal(JtJ, dim1=1, dim2=2), pose)
-        _, JtR_s = ic.iterate_poses(R_s, t_s, x0, x1, invD0, invD1, K, None, None,
-                                    no_uncertainty=True, weights=weights, obj_mask1=obj_mask1)
+        if replicated is not None:
+            xs0, xs1, ds0, ds1, Ks, ws, ms1 = replicated
+            _, _, _, JtR_s, _ = ic.iterate((R_s.view(S * B, 3, 3), t_s.view(S * B, 3, 1)), xs0, xs1, ds0, ds1, Ks,
+                                           None, None, first=False, update=False, no_uncertainty=True, weights=ws,
+                                           obj_mask1=ms1)
+            JtR_s = JtR_s.view(S, B, 6)
+        else:
+            _, JtR_s = ic.iterate_poses(R_s, t_s, x0, x1, invD0, invD1, K, None, None,
+                                        no_uncertainty=True, weights=weights, obj_mask1=obj_mask1)
         JtR_flat = JtR_s.permute(1, 2, 0).reshape(B, -1)  # [B, 6, S]: as the reference's cat(dim=2)
         damp = self.net(torch.cat((JtR_flat, JtJ.view(B, -1)), dim=1))
         R1, t1 = ic.damped_update(JtJ, JtR, damp.view(1, B, 6), pose)
@@ -443,10 +461,12 @@ class TrustRegionBase(nn.Module):
         resvol = getattr(self.directSolver, 'type', 0) == DirectSolverNet.SOLVER_RESIDUAL_VOLUME
         with torch.no_grad():
             w, _, _ = self._weights(pose, x0, x1, invD0, invD1, K, wPrior, obj_mask0, obj_mask1)
+            rep = self.directSolver.replicate((x0, x1, invD0, invD1, K), w, obj_mask1) if resvol else None
             for it in range(self.max_iterations):
                 m0 = obj_mask0 if it == 0 else None
                 if resvol:
                     pose = self.directSolver.resvol_step(pose, (x0, x1, invD0, invD1, K), w, m0, obj_mask1,
+                                                         replicated=rep,
                                                          first=(it == 0))
                 else:
                     R, t, _, _, _ = ic.iterate(pose, x0, x1, invD0, invD1, K, None, None, first=(it == 0),
