@@ -2585,6 +2585,20 @@ __global__ __launch_bounds__(kThreads) void pack_c4_kernel(const float* __restri
   dst[i] = f32x4{s[0], s[HW], s[2 * (long)HW], s[3 * (long)HW]};
 }
 
+// NHWC (channels_last) -> channel-quad layout: thread r of pair row b = blockIdx.y reads
+// the 16-byte quad r of the pair's [HW][C] block (a linear, coalesced read) and writes it
+// to plane q = r % Q at pixel r / Q (64 lanes = 64 / Q pixels x Q planes: one 128-byte run
+// per plane for Q = 8).
+__global__ __launch_bounds__(kThreads) void pack_c4_nhwc_kernel(const f32x4* __restrict__ src,
+                                                                f32x4* __restrict__ dst, uint32_t n, uint32_t Q,
+                                                                uint32_t HW) {
+  const uint32_t r = blockIdx.x * kThreads + threadIdx.x;
+  if (r >= n) return;
+  const size_t base = (size_t)blockIdx.y * n;
+  const uint32_t pix = r / Q, q = r - pix * Q;
+  dst[base + (size_t)q * HW + pix] = __builtin_nontemporal_load(src + base + r);
+}
+
 // sigma0 batch-global min / max (algorithms.py:1976-1977).  Per-workgroup
 // partials, the last workgroup reduces them in a fixed order (no atomics on data).
 __device__ void minmax_body(const float* __restrict__ s, size_t n, uint32_t* ctrl, int slot, float* part,
@@ -3567,6 +3581,20 @@ int dpft_pack_features(const float* src, float* dst, int32_t B, int32_t C, int32
   hipLaunchKernelGGL(pack_c4_kernel, dim3((unsigned)((n + kThreads - 1) / kThreads)), dim3(kThreads), 0,
                      static_cast<hipStream_t>(hip_stream), src, reinterpret_cast<f32x4*>(dst), n, H * W);
   return hip_check("pack_c4_kernel");
+}
+
+int dpft_pack_features_nhwc(const float* src, float* dst, int32_t B, int32_t C, int32_t H, int32_t W,
+                            void* hip_stream) {
+  if (!src || !dst || src == dst) return fail(DPFT_E_INVALID, "null or aliased pointer");
+  if (B < 1 || B > 65535 || C < 4 || C % 4 != 0 || H < 1 || W < 1 || (long)H * W * (C / 4) >= (1L << 31))
+    return fail(DPFT_E_INVALID, "bad shape B=%d C=%d H=%d W=%d (C %% 4 == 0 needed)", B, C, H, W);
+  if ((reinterpret_cast<uintptr_t>(src) | reinterpret_cast<uintptr_t>(dst)) & 15)
+    return fail(DPFT_E_INVALID, "src / dst must be 16-byte aligned");
+  const uint32_t Q = (uint32_t)(C / 4), HW = (uint32_t)H * (uint32_t)W, n = HW * Q;
+  hipLaunchKernelGGL(pack_c4_nhwc_kernel, dim3((n + kThreads - 1) / kThreads, (unsigned)B), dim3(kThreads), 0,
+                     static_cast<hipStream_t>(hip_stream), reinterpret_cast<const f32x4*>(src),
+                     reinterpret_cast<f32x4*>(dst), n, Q, HW);
+  return hip_check("pack_c4_nhwc_kernel");
 }
 
 int dpft_version(void) { return DPFT_ABI_VERSION; }

@@ -70,12 +70,24 @@ def pack_features(x):
         raise RuntimeError("pack_features needs a device tensor; there is no CPU fallback")
     if x.dtype != torch.float32 or x.dim() != 4 or x.shape[1] % 4 != 0:
         raise ValueError(f"need fp32 [B,C,H,W] with C % 4 == 0, got {x.dtype} {tuple(x.shape)}")
-    x = x.contiguous()
     B, C, H, W = x.shape
     out = torch.empty(B, C // 4, H, W, 4, dtype=torch.float32, device=x.device)
+    if channels_last(x):  # NHWC storage: one relayout pass (dpft_pack_features_nhwc)
+        if x.data_ptr() % 16:
+            x = x.contiguous(memory_format=torch.channels_last)
+        rc = N.lib().dpft_pack_features_nhwc(_ptr(x), _ptr(out), B, C, H, W, _stream(x.device))
+        N.check(rc, "dpft_pack_features_nhwc")
+        return out
+    x = x.contiguous()
     rc = N.lib().dpft_pack_features(_ptr(x), _ptr(out), B, C, H, W, _stream(x.device))
     N.check(rc, "dpft_pack_features")
     return out
+
+
+def channels_last(x):
+    """True for a 4-D map stored channels_last (NHWC) rather than NCHW -- the encoder's
+    output when it runs in torch.channels_last memory format."""
+    return x.dim() == 4 and not x.is_contiguous() and x.is_contiguous(memory_format=torch.channels_last)
 
 
 def unpack_features(xp):
@@ -107,8 +119,9 @@ def feature_shape(x):
 class LevelCall:
     """Validated, pointer-ready arguments of one pyramid level.
 
-    x0 / x1 are [B,C,H,W] (NCHW) or channel-quad packed [B,C/4,H,W,4]; with
-    pack=True eligible NCHW inputs are packed here (once for all iterations).
+    x0 / x1 are [B,C,H,W] (NCHW or channels_last) or channel-quad packed
+    [B,C/4,H,W,4]; eligible inputs are packed here (once for all iterations) when
+    pack=True or when they are stored channels_last.
     schedule (None = "auto", "march", "split") forces the channel-quad
     reduce kernel (include/dpft_ic.h, DPFT_SCHED_*); it changes only the order in
     which the per-pixel sums are added."""
@@ -125,7 +138,9 @@ class LevelCall:
                 raise ValueError(f"{name} is on {t.device}, expected {x0.device}")
         if x1.shape != x0.shape:
             raise ValueError(f"x1 {tuple(x1.shape)} != x0 {tuple(x0.shape)}")
-        if pack and packable(x0, sigma0, no_uncertainty):
+        # channels_last maps need a relayout pass either way: make it the one to the
+        # channel-quad layout (the faster solve) whenever the level is packable
+        if packable(x0, sigma0, no_uncertainty) and (pack or channels_last(x0) or channels_last(x1)):
             x0, x1 = pack_features(x0), pack_features(x1)
         c4 = x0.dim() == 5
         B, C, H, W = feature_shape(x0)

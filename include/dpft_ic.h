@@ -250,6 +250,14 @@ int dpft_preprocess_depth(const float* depth, int32_t B, int32_t H, int32_t W, i
 int dpft_pack_features(const float* src, float* dst, int32_t B, int32_t C, int32_t H, int32_t W, void* hip_stream);
 
 /*
+ * The same relayout from a channels_last map: src [B,H,W,C] (NHWC; the encoder run in
+ * channels_last memory format, `torch.channels_last`) -> dst [B,C/4,H,W,4].  One pass,
+ * instead of a transposition to NCHW followed by dpft_pack_features.  16-byte aligned.
+ */
+int dpft_pack_features_nhwc(const float* src, float* dst, int32_t B, int32_t C, int32_t H, int32_t W,
+                            void* hip_stream);
+
+/*
  * Jacobian API, materialised -- the reference solver's methods that the fused solve
  * never needs (it keeps J in registers); kept for callers and tests that inspect J.
  *  dpft_feature_gradient    feature_gradient (algorithms.py:1844-1865): unit-normalised

@@ -57,6 +57,34 @@ def test_pack_round_trip_bit_exact(B, C, H, W):
     assert torch.equal(ic.unpack_features(p), x)
 
 
+@pytest.mark.parametrize("B,C,H,W", [(2, 8, 37, 70), (1, 32, 120, 160), (3, 4, 5, 3), (2, 16, 6, 10), (8, 32, 60, 80)])
+def test_pack_channels_last_bit_exact(B, C, H, W):
+    """A channels_last map packs (dpft_pack_features_nhwc) to the same bytes as its
+    NCHW copy, and a solve handed the channels_last maps runs the channel-quad path on
+    them: the same poses, bit for bit, as one handed the packed maps."""
+    from deep_prob_feature_track_amd import ic
+    dev = _dev()
+    x = torch.randn(B, C, H, W, device=dev)
+    xl = x.contiguous(memory_format=torch.channels_last)
+    assert ic.channels_last(xl) and not ic.channels_last(x)
+    assert torch.equal(ic.pack_features(xl), ic.pack_features(x))
+    if H < 16:
+        return
+    f1 = torch.roll(x, shifts=(1, 2), dims=(2, 3)) + 0.01 * torch.randn(B, C, H, W, device=dev)
+    s0 = 0.5 + torch.rand(B, 1, H, W, device=dev)
+    s1 = 0.5 + torch.rand(B, 1, H, W, device=dev)
+    d0 = 0.2 + torch.rand(B, 1, H, W, device=dev)
+    d1 = 0.2 + torch.rand(B, 1, H, W, device=dev)
+    K = torch.tensor([[W * 0.8, W * 0.8, (W - 1) / 2, (H - 1) / 2]], device=dev).repeat(B, 1)
+    pose = (torch.eye(3, device=dev).repeat(B, 1, 1), torch.zeros(B, 3, 1, device=dev))
+    sig0, sig1 = s0.expand(B, C, H, W), s1.expand(B, C, H, W)
+    ra = ic.solve_level(pose, ic.pack_features(x), ic.pack_features(f1), d0, d1, K, sig0, sig1, iters=3,
+                        remove_tru_sigma=True)
+    rb = ic.solve_level(pose, xl, f1.contiguous(memory_format=torch.channels_last), d0, d1, K, sig0, sig1,
+                        iters=3, remove_tru_sigma=True)
+    assert torch.equal(ra[0], rb[0]) and torch.equal(ra[1], rb[1])
+
+
 @pytest.mark.parametrize("name", ["cfg1_160x120_c8", "batch4_160x120_c8", "masks_160x120_c8",
                                   "cfg2_640x480_c32", "icp_160x120_c8"])
 def test_c4_equals_nchw_and_golden(name):
