@@ -3468,6 +3468,39 @@ __global__ __launch_bounds__(kThreads) void read_probe_kernel(const f32x4* __res
   for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off);
   if ((threadIdx.x & 63) == 0) out[blockIdx.x * (kThreads / 64) + (threadIdx.x >> 6)] = v;
 }
+
+// Encoder block epilogue in eval mode (submodules.py convLayer: BatchNorm2d with running
+// statistics, then ELU(alpha = 1)): y = x * a_c + b_c with a = w / sqrt(var + eps),
+// b = bias - mean * a (the linear form ATen's CPU inference applies), then
+// y > 0 ? y : expm1(y), in place, one 16-byte read and write per four values (two
+// elementwise passes in the torch modules).  chan = [a | b], C floats each.  NHWC: the
+// four values of a 16-byte unit are channels c .. c + 3 (C % 4 == 0); NCHW: one channel
+// (H W % 4 == 0).
+__device__ inline float bn_elu1(float x, const float* __restrict__ chan, uint32_t C, uint32_t c) {
+  const float y = x * chan[c] + chan[C + c];
+  return y > 0.0f ? y : expm1f(y);
+}
+template <bool NHWC>
+__global__ __launch_bounds__(kThreads) void bn_elu_kernel(f32x4* __restrict__ x, const float* __restrict__ chan,
+                                                          uint32_t n4, uint32_t C, uint32_t inner4) {
+  const uint32_t i = blockIdx.x * kThreads + threadIdx.x;
+  if (i >= n4) return;
+  f32x4 v = x[i];
+  if (NHWC) {
+    const uint32_t c = (i % (C / 4)) * 4;
+    v.x = bn_elu1(v.x, chan, C, c);
+    v.y = bn_elu1(v.y, chan, C, c + 1);
+    v.z = bn_elu1(v.z, chan, C, c + 2);
+    v.w = bn_elu1(v.w, chan, C, c + 3);
+  } else {
+    const uint32_t c = (i / inner4) % C;
+    v.x = bn_elu1(v.x, chan, C, c);
+    v.y = bn_elu1(v.y, chan, C, c);
+    v.z = bn_elu1(v.z, chan, C, c);
+    v.w = bn_elu1(v.w, chan, C, c);
+  }
+  x[i] = v;
+}
 }  // namespace
 
 extern "C" {
@@ -3595,6 +3628,25 @@ int dpft_pack_features_nhwc(const float* src, float* dst, int32_t B, int32_t C, 
                      static_cast<hipStream_t>(hip_stream), reinterpret_cast<const f32x4*>(src),
                      reinterpret_cast<f32x4*>(dst), n, Q, HW);
   return hip_check("pack_c4_nhwc_kernel");
+}
+
+int dpft_bn_elu(float* x, const float* chan, int64_t n, int32_t C, int64_t inner, int32_t nhwc, void* hip_stream) {
+  if (!x || !chan) return fail(DPFT_E_INVALID, "null pointer");
+  if (n < 4 || C < 1 || inner < 1 || n % 4 != 0 || n / 4 >= (1L << 32) - kThreads || n % (C * inner) != 0)
+    return fail(DPFT_E_INVALID, "bad size n=%ld C=%d inner=%ld", (long)n, C, (long)inner);
+  if (reinterpret_cast<uintptr_t>(x) & 15) return fail(DPFT_E_INVALID, "x must be 16-byte aligned");
+  if (nhwc ? (C % 4 != 0 || inner != 1) : (inner % 4 != 0))
+    return fail(DPFT_E_INVALID, "the 16-byte units must not straddle channels (C=%d inner=%ld)", C, (long)inner);
+  const uint32_t n4 = (uint32_t)(n / 4);
+  const dim3 grid((n4 + kThreads - 1) / kThreads);
+  const hipStream_t st = static_cast<hipStream_t>(hip_stream);
+  f32x4* x4 = reinterpret_cast<f32x4*>(x);
+  if (nhwc)
+    hipLaunchKernelGGL(bn_elu_kernel<true>, grid, dim3(kThreads), 0, st, x4, chan, n4, (uint32_t)C, 1u);
+  else
+    hipLaunchKernelGGL(bn_elu_kernel<false>, grid, dim3(kThreads), 0, st, x4, chan, n4, (uint32_t)C,
+                       (uint32_t)(inner / 4));
+  return hip_check("bn_elu_kernel");
 }
 
 int dpft_version(void) { return DPFT_ABI_VERSION; }

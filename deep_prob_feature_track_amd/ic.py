@@ -84,6 +84,49 @@ def pack_features(x):
     return out
 
 
+def _bn_coeffs(bn, device):
+    """[a | b] (2C fp32 on `device`) of an eval-mode BatchNorm2d: a = w / sqrt(var + eps),
+    b = bias - mean * a.  Cached on the module until its statistics or affine parameters
+    change (in-place updates such as load_state_dict bump the tensor versions)."""
+    ts = [bn.running_mean, bn.running_var] + ([bn.weight, bn.bias] if bn.affine else [])
+    key = (device,) + tuple(t._version for t in ts) + tuple(t.data_ptr() for t in ts)
+    hit = getattr(bn, "_dpft_coeffs", None)
+    if hit is not None and hit[0] == key:
+        return hit[1]
+    with torch.no_grad():
+        a = 1.0 / torch.sqrt(bn.running_var.float() + bn.eps)
+        if bn.affine:
+            a = a * bn.weight.float()
+        b = -bn.running_mean.float() * a
+        if bn.affine:
+            b = b + bn.bias.float()
+        chan = torch.cat((a, b)).to(device=device, dtype=torch.float32).contiguous()
+    bn._dpft_coeffs = (key, chan)
+    return chan
+
+
+def bn_elu_(x, bn):
+    """In place x = ELU(bn(x)) for an eval-mode BatchNorm2d with running statistics
+    (the reference's convLayer epilogue, submodules.py:25-39) in one pass
+    (dpft_bn_elu).  Returns False, x untouched, when x's layout does not fit the kernel
+    (the caller then runs the two torch modules)."""
+    if not x.is_cuda or x.dtype != torch.float32 or x.dim() != 4 or bn.running_mean is None:
+        return False
+    B, C, H, W = x.shape
+    if channels_last(x):
+        nhwc, inner, ok = 1, 1, C % 4 == 0
+    elif x.is_contiguous():
+        nhwc, inner, ok = 0, H * W, (H * W) % 4 == 0
+    else:
+        return False
+    if not ok or x.data_ptr() % 16 or C != bn.num_features:
+        return False
+    chan = _bn_coeffs(bn, x.device)
+    rc = N.lib().dpft_bn_elu(_ptr(x), _ptr(chan), x.numel(), C, inner, nhwc, _stream(x.device))
+    N.check(rc, "dpft_bn_elu")
+    return True
+
+
 def channels_last(x):
     """True for a 4-D map stored channels_last (NHWC) rather than NCHW -- the encoder's
     output when it runs in torch.channels_last memory format."""

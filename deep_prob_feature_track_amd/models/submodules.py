@@ -10,6 +10,8 @@ import torch
 import torch.nn as nn
 from torch.nn import init
 
+from .. import ic
+
 _RGB_MEAN = (0.4914, 0.4822, 0.4465)
 _RGB_STD = (0.2023, 0.1994, 0.2010)
 
@@ -34,6 +36,23 @@ def _padding(kernel_size, dilation):
     return (kernel_size - 1) // 2 + dilation - 1
 
 
+class ConvBlock(nn.Sequential):
+    """conv [-> batchnorm] -> ELU, an nn.Sequential (the reference's state_dict keys).
+    In eval mode on the GPU, outside autograd, the batchnorm and the ELU of a 2-D block
+    run as one in-place pass over the conv output (`ic.bn_elu_`, dpft_bn_elu) instead of
+    two elementwise kernels; otherwise, or for a layout the kernel does not take, the
+    modules run in turn."""
+
+    def forward(self, x):
+        if len(self) == 3 and isinstance(self[1], nn.BatchNorm2d) and isinstance(self[2], nn.ELU) \
+                and self[2].alpha == 1.0 and not self.training and x.is_cuda and not torch.is_grad_enabled():
+            y = self[0](x)
+            if ic.bn_elu_(y, self[1]):
+                return y
+            return self[2](self[1](y))
+        return super().forward(x)
+
+
 def _block(conv_cls, bn_cls, batch_norm, cin, cout, kernel_size, stride, dilation, bias):
     layers = [conv_cls(cin, cout, kernel_size=kernel_size, stride=stride,
                        padding=_padding(kernel_size, dilation), dilation=dilation,
@@ -41,7 +60,7 @@ def _block(conv_cls, bn_cls, batch_norm, cin, cout, kernel_size, stride, dilatio
     if batch_norm:
         layers.append(bn_cls(cout))
     layers.append(nn.ELU(inplace=True))
-    return nn.Sequential(*layers)
+    return ConvBlock(*layers)
 
 
 def convLayer(batchNorm, in_planes, out_planes, kernel_size=3, stride=1, dilation=1, bias=False):

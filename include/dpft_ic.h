@@ -258,6 +258,16 @@ int dpft_pack_features_nhwc(const float* src, float* dst, int32_t B, int32_t C, 
                             void* hip_stream);
 
 /*
+ * Encoder block epilogue in eval mode (reference submodules.py:25-39, convLayer:
+ * conv -> BatchNorm2d(running statistics) -> ELU), in place on the conv output x of n
+ * floats: x = elu(x * a[c] + b[c]) with a = weight / sqrt(running_var + eps),
+ * b = bias - running_mean * a (chan = [a | b], 2C floats, device).  nhwc = 1: x is
+ * channels_last (channel = index % C; C % 4 == 0, inner = 1); nhwc = 0: NCHW with inner =
+ * H*W (channel = index / inner % C; inner % 4 == 0).  x 16-byte aligned.
+ */
+int dpft_bn_elu(float* x, const float* chan, int64_t n, int32_t C, int64_t inner, int32_t nhwc, void* hip_stream);
+
+/*
  * Jacobian API, materialised -- the reference solver's methods that the fused solve
  * never needs (it keeps J in registers); kept for callers and tests that inspect J.
  *  dpft_feature_gradient    feature_gradient (algorithms.py:1844-1865): unit-normalised

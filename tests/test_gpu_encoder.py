@@ -1,0 +1,89 @@
+"""Encoder block epilogue (dpft_bn_elu) and the channels_last encoder on a real MI355X
+(`-m gpu`): the fused in-place batchnorm + ELU pass against the torch modules it
+replaces (reference submodules.py:25-39, convLayer), in both memory formats."""
+import pytest
+import torch
+import torch.nn as nn
+
+pytestmark = pytest.mark.gpu
+
+
+def _dev():
+    if not torch.cuda.is_available():
+        pytest.skip("no HIP device")
+    return torch.device("cuda:0")
+
+
+def _block(cin, cout, k, dil, dev, seed):
+    from deep_prob_feature_track_amd.models.submodules import convLayer
+    torch.manual_seed(seed)
+    blk = convLayer(True, cin, cout, k, dilation=dil)
+    bn = blk[1]
+    with torch.no_grad():  # non-trivial running statistics and affine terms
+        bn.running_mean.uniform_(-0.5, 0.5)
+        bn.running_var.uniform_(0.2, 3.0)
+        bn.weight.uniform_(0.5, 1.5)
+        bn.bias.uniform_(-0.3, 0.3)
+    return blk.to(dev).eval()
+
+
+@pytest.mark.parametrize("cin,cout,k,dil,H,W", [(8, 16, 3, 1, 48, 64), (16, 32, 3, 2, 30, 40), (32, 32, 1, 1, 7, 9),
+                                                (3, 6, 3, 1, 10, 10)])
+@pytest.mark.parametrize("nhwc", [False, True])
+def test_bn_elu_matches_torch_modules(cin, cout, k, dil, H, W, nhwc):
+    from deep_prob_feature_track_amd import ic
+    dev = _dev()
+    blk = _block(cin, cout, k, dil, dev, seed=cin + cout + H)
+    x = torch.randn(2, cin, H, W, device=dev)
+    if nhwc:
+        blk = blk.to(memory_format=torch.channels_last)
+        x = x.contiguous(memory_format=torch.channels_last)
+    with torch.no_grad():
+        conv = blk[0](x)
+        ref = nn.functional.elu(nn.functional.batch_norm(conv, blk[1].running_mean, blk[1].running_var,
+                                                         blk[1].weight, blk[1].bias, False, 0.0, blk[1].eps))
+        y = conv.clone()
+        fused = ic.bn_elu_(y, blk[1])
+        out = blk(x)  # ConvBlock.forward: fused where the layout allows, the modules otherwise
+    # (H W % 4 != 0 in NCHW, C % 4 != 0 in NHWC: the kernel declines and the modules run)
+    assert fused == ((cout % 4 == 0) if nhwc else ((H * W) % 4 == 0))
+    if fused:
+        torch.testing.assert_close(y, ref, rtol=2e-6, atol=2e-6)
+    torch.testing.assert_close(out, ref, rtol=2e-6, atol=2e-6)
+    assert out.is_contiguous(memory_format=torch.channels_last if nhwc else torch.contiguous_format)
+
+
+def test_bn_coefficients_follow_state_dict_loads():
+    """The cached [a | b] coefficients are rebuilt after load_state_dict changes the
+    statistics (tensor versions move)."""
+    dev = _dev()
+    blk = _block(8, 16, 3, 1, dev, seed=3)
+    x = torch.randn(1, 8, 16, 16, device=dev)
+    with torch.no_grad():
+        y0 = blk(x)
+        sd = {k: v.clone() for k, v in blk.state_dict().items()}
+        sd["1.running_var"] = sd["1.running_var"] * 4.0
+        blk.load_state_dict(sd)
+        y1 = blk(x)
+        conv = blk[0](x)
+        ref = nn.functional.elu(nn.functional.batch_norm(conv, blk[1].running_mean, blk[1].running_var,
+                                                         blk[1].weight, blk[1].bias, False, 0.0, blk[1].eps))
+    assert not torch.allclose(y0, y1)
+    torch.testing.assert_close(y1, ref, rtol=2e-6, atol=2e-6)
+
+
+def test_channels_last_encoder_matches_nchw():
+    """The drop-in's channels_last encoder gives the NCHW encoder's features (MIOpen's
+    NHWC convolutions sum in another order: fp32 rounding only)."""
+    from deep_prob_feature_track_amd.models.algorithms import FeaturePyramid
+    dev = _dev()
+    torch.manual_seed(0)
+    enc = FeaturePyramid(D=8, w_uncertainty="laplacian", feature_channel=8, feature_extract="conv",
+                         uncertainty_channel=1).to(dev).eval()
+    x = torch.randn(2, 8, 60, 80, device=dev)
+    with torch.no_grad():
+        f_a, s_a, _ = enc(x)
+        enc.to(memory_format=torch.channels_last)
+        f_b, s_b, _ = enc(x.contiguous(memory_format=torch.channels_last))
+    for a, b in zip(f_a + s_a, f_b + s_b):
+        torch.testing.assert_close(b, a, rtol=1e-4, atol=1e-5 * a.abs().max().item())
