@@ -83,14 +83,18 @@ def make_inputs(B, rank, device):
 def l0_traffic():
     """Per-launch HBM bytes of the level-0 reduce launch from the committed PMC
     measurement (tools/pmc_l0.py: separate FETCH_SIZE / WRITE_SIZE rocprofv3 passes,
-    gfx950-corrected), used only if it was measured on the kernel source built here."""
+    gfx950-corrected), used only if it was measured on the machine code of the kernel
+    built here (the ISA hash build.py records beside the library; the source file's hash
+    for measurements that predate it)."""
     import glob
     import hashlib
+    from deep_prob_feature_track_amd import build as B
     src = os.path.join(ROOT, "deep_prob_feature_track_amd", "csrc", "dpft_ic.hip")
     sha = hashlib.sha256(open(src, "rb").read()).hexdigest()
+    isa = json.load(open(B.ISA_OUT)).get(B.L0_KERNEL) if os.path.exists(B.ISA_OUT) else None
     for f in sorted(glob.glob(os.path.join(ROOT, "profiles", "*_l0_traffic.json")), reverse=True):
         d = json.load(open(f))
-        if d.get("src_sha256") == sha:
+        if (isa is not None and d.get("isa_sha256") == isa) or d.get("src_sha256") == sha:
             return {"hbm_bytes": d["hbm_bytes"], "source": os.path.relpath(f, ROOT)}
     return None
 

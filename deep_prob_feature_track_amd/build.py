@@ -59,9 +59,51 @@ def check_occupancy(res):
         raise RuntimeError("occupancy regression:\n  " + "\n  ".join(bad))
 
 
+LLVM_BIN = "/opt/rocm/lib/llvm/bin"
+ISA_OUT = os.path.join(HERE, "libdpft_ic.isa.json")
+# the level-0/1 marching kernel of the bench (C = 32, one sigma plane, remove_tru_sigma, U_IC, channel quads)
+L0_KERNEL = "_ZN12_GLOBAL__N_116ic_reduce_kernelILi32ELb1ELb1ELi0ELb1EEEvNS_10IterParamsE"
+
+
+def isa_hashes(so_path=OUT):
+    """{mangled kernel name: SHA-256 of its gfx950 instruction text} from the library's
+    device code object (llvm-objdump; addresses and encodings dropped, branch offsets are
+    relative).  A per-launch PMC measurement names the hash of the kernel it measured, so
+    it stays valid while that kernel's machine code is unchanged, whatever else changes
+    in the source file."""
+    import hashlib
+    import tempfile
+    with tempfile.TemporaryDirectory() as d:
+        fb, co = os.path.join(d, "fb.bin"), os.path.join(d, "co.o")
+        subprocess.run([os.path.join(LLVM_BIN, "llvm-objcopy"), f"--dump-section=.hip_fatbin={fb}", so_path, os.path.join(d, "x.so")],
+                       check=True, capture_output=True)
+        subprocess.run([os.path.join(LLVM_BIN, "clang-offload-bundler"), "--unbundle", "--type=o", f"--input={fb}",
+                        f"--targets=hipv4-amdgcn-amd-amdhsa--{ARCH}", f"--output={co}"], check=True, capture_output=True)
+        dis = subprocess.run([os.path.join(LLVM_BIN, "llvm-objdump"), "-d", "--no-show-raw-insn", "--no-leading-addr", co],
+                             check=True, capture_output=True, text=True).stdout
+    out, name, body = {}, None, []
+    for line in dis.splitlines() + ["<end>:"]:
+        m = re.match(r"^<(\S+)>:$", line)
+        if m:
+            if name is not None:
+                out[name] = hashlib.sha256("\n".join(body).encode()).hexdigest()
+            name, body = m.group(1), []
+        elif name is not None and line.strip():
+            body.append(line.split("//")[0].strip())
+    out.pop("end", None)
+    return out
+
+
+def write_isa_hashes():
+    import json
+    json.dump(isa_hashes(OUT), open(ISA_OUT, "w"), indent=0, sort_keys=True)
+
+
 def build(force=False, verbose=False):
     deps = [SRC, os.path.join(INC, "dpft_ic.h"), __file__]
     if not force and os.path.exists(OUT) and os.path.getmtime(OUT) >= max(os.path.getmtime(d) for d in deps):
+        if not os.path.exists(ISA_OUT) or os.path.getmtime(ISA_OUT) < os.path.getmtime(OUT):
+            write_isa_hashes()
         return OUT
     cmd = [HIPCC, f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-shared", "-fPIC", f"-I{INC}",
            "-Rpass-analysis=kernel-resource-usage", "-o", OUT + ".tmp", SRC]
@@ -73,6 +115,7 @@ def build(force=False, verbose=False):
         raise subprocess.CalledProcessError(r.returncode, cmd)
     check_occupancy(kernel_resources(r.stderr))
     os.replace(OUT + ".tmp", OUT)
+    write_isa_hashes()
     return OUT
 
 

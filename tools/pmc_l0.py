@@ -9,8 +9,8 @@ under two separate `rocprofv3 --pmc` passes (FETCH_SIZE; WRITE_SIZE) and writes 
 per-launch bytes, corrected as MI355X_MICROARCH.md's HBM section prescribes:
 FETCH_SIZE counts half the bytes of a 128-B-request stream on gfx950 (TCC_EA0_RDREQ
 x 64 B) -> read bytes = 2 x 1024 x FETCH_SIZE; WRITE_SIZE (KiB) is exact.  The
-JSON carries the SHA-256 of the kernel source, so bench.py uses it only while the
-source it was measured on is unchanged.
+JSON carries the SHA-256 of the measured kernel's machine code (and of the source file),
+so bench.py uses it only while that kernel's code is unchanged.
 """
 import argparse
 import csv
@@ -30,6 +30,14 @@ SOLVE_LAUNCHES = 6
 
 def src_sha():
     return hashlib.sha256(open(SRC, "rb").read()).hexdigest()
+
+
+def isa_sha():
+    """Hash of the measured kernel's machine code (deep_prob_feature_track_amd/build.py)."""
+    sys.path.insert(0, ROOT)
+    from deep_prob_feature_track_amd import build as B
+    lib = os.environ.get("DPFT_LIB")
+    return (B.isa_hashes(os.path.abspath(lib)) if lib else json.load(open(B.ISA_OUT))).get(B.L0_KERNEL)
 
 
 def run_pass(counter, outdir):
@@ -61,7 +69,7 @@ def main():
     fetch, nf = run_pass("FETCH_SIZE", os.path.join(tmp, "fetch"))
     write, nw = run_pass("WRITE_SIZE", os.path.join(tmp, "write"))
     out = {"kernel": "ic_reduce_kernel<32,Cs=1,tru,U_IC,c4> level 0, B=8, 640x480 (tools/kbench.py --mode level --from-solve)",
-           "src_sha256": src_sha(), "launches": {"fetch": nf, "write": nw},
+           "src_sha256": src_sha(), "isa_sha256": isa_sha(), "launches": {"fetch": nf, "write": nw},
            "FETCH_SIZE_KiB": fetch, "WRITE_SIZE_KiB": write,
            "read_bytes": 2 * 1024 * fetch, "write_bytes": 1024 * write,
            "hbm_bytes": 2 * 1024 * fetch + 1024 * write,
