@@ -2,18 +2,20 @@
 """Benchmark: IC solver iterations/s, 640x480, C=32, 4-level pyramid (BASELINE.json).
 
 One *step* = one full coarse-to-fine solve (levels 3..0, 3 Gauss-Newton
-iterations each = 12 IC iterations per pair) of a batch of B frame pairs per
-GPU, replayed from one HIP graph, followed (N > 1) by the RCCL all-gather of
-the per-pair poses.  An eval stream keeps --inflight batches (default 4, distinct
-pairs each) in flight per GPU: step k replays slot k % inflight's graph on that
-slot's stream, so one batch's latency-bound coarse levels overlap another's
-bandwidth-bound level 0; every batch is solved exactly as alone (batch-global
-masks over its own B pairs, bit-identical poses).  `latency_ms_per_solve` is one
-solve with nothing else in flight.  Workload: cfg3's shard -- B = 8 pairs per GPU cycled from
-the ordered pairs of the five TUM fr1/desk frames, deterministic features
+iterations each = 12 IC iterations per pair) of G independent batches of B frame
+pairs per GPU (--groups G, --batch-per-gpu B), replayed from one HIP graph, followed
+(N > 1) by the RCCL all-gather of the per-pair poses.  The G batches share every
+launch (DPFT_GROUP: each batch keeps its own batch-global truncated-sigma extrema and
+is solved exactly as a call of its own), so the per-launch ramp, finish spread and
+finalize are paid once per G batches.  An eval stream keeps --inflight such grouped
+solves in flight per GPU (distinct pairs each): step k replays slot k % inflight's
+graph on that slot's stream, so one solve's latency-bound coarse levels overlap
+another's bandwidth-bound level 0.  `latency_ms_per_solve` is one grouped solve with
+nothing else in flight.  Workload: cfg3's shard -- B = 8 pairs per GPU per batch,
+cycled from the ordered pairs of the five TUM fr1/desk frames, deterministic features
 (tests/golden/recipe.py), inputs resident in HBM before the timed region.
 
-`value` = all-level IC iterations/s over the whole job = N * B * 12 / step time.
+`value` = all-level IC iterations/s over the whole job = N * G * B * 12 / step time.
 Launch: python bench.py [--gpus N --steps K --warmup W]; for N > 1 under
 torch.distributed.run (one rank per GPU, RCCL).
 """
@@ -43,9 +45,11 @@ def parse():
     p.add_argument("--setup-warm-ms", type=float, default=200.0,
                    help="setup: replay solves for this long before the --warmup steps (the GPU clock ramps over "
                         "the first tens of milliseconds of load; 5 warm-up steps are 3 ms)")
+    p.add_argument("--groups", type=int, default=4,
+                   help="independent B-pair batches per launch (DPFT_GROUP): each solved as its own call -- its "
+                        "own batch-global truncated-sigma extrema -- in launches covering all of them")
     p.add_argument("--inflight", type=int, default=4,
-                   help="independent B-pair batches in flight per GPU (one stream, graph, workspace and input "
-                        "set each; each batch's solve is unchanged, bit for bit)")
+                   help="grouped solves in flight per GPU (one stream, graph, workspace and input set each)")
     p.add_argument("--kernel-reps", type=int, default=50)
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--no-graph", action="store_true")
@@ -53,6 +57,17 @@ def parse():
                    help="resident feature layout the timed solve reads (c4: channel-quad, the solver's native one)")
     p.add_argument("--no-compare", action="store_true", help="skip the secondary timing of the other layout")
     return p.parse_args()
+
+
+def make_group_inputs(B, G, first, device):
+    """G independent B-pair batches (make_inputs `first` .. `first` + G - 1) stacked along
+    the pair axis: batch g is pairs [g B, (g + 1) B) of one DPFT_GROUP(B) call."""
+    parts = [make_inputs(B, first + g, device) for g in range(G)]
+    if G == 1:
+        return parts[0]
+    sel = [p for part in parts for p in part[0]]
+    levels = [{k: torch.cat([part[1][l][k] for part in parts]) for k in parts[0][1][l]} for l in range(LEVELS)]
+    return sel, levels, torch.cat([part[2] for part in parts])
 
 
 def make_inputs(B, rank, device):
@@ -80,7 +95,7 @@ def make_inputs(B, rank, device):
     return sel, levels, K
 
 
-def l0_traffic():
+def l0_traffic(pairs, group):
     """Per-launch HBM bytes of the level-0 reduce launch from the committed PMC
     measurement (tools/pmc_l0.py: separate FETCH_SIZE / WRITE_SIZE rocprofv3 passes,
     gfx950-corrected), used only if it was measured on the machine code of the kernel
@@ -94,6 +109,8 @@ def l0_traffic():
     isa = json.load(open(B.ISA_OUT)).get(B.L0_KERNEL) if os.path.exists(B.ISA_OUT) else None
     for f in sorted(glob.glob(os.path.join(ROOT, "profiles", "*_l0_traffic.json")), reverse=True):
         d = json.load(open(f))
+        if d.get("pairs_per_launch", 8) != pairs or d.get("group", pairs) != group:
+            continue  # measured on another launch shape
         if (isa is not None and d.get("isa_sha256") == isa) or d.get("src_sha256") == sha:
             return {"hbm_bytes": d["hbm_bytes"], "source": os.path.relpath(f, ROOT)}
     return None
@@ -222,10 +239,12 @@ def main():
     from deep_prob_feature_track_amd import ic, shard
 
     B = a.batch_per_gpu
+    G = max(1, a.groups)
     S = max(1, a.inflight)
-    # batch j of this rank: the pairs of make_inputs "rank" rank * S + j (distinct pairs per
-    # in-flight slot and rank, cycled through the 20 ordered pairs of the 5 frames)
-    slot_inputs = [make_inputs(B, rank * S + j, device) for j in range(S)]
+    BG = B * G  # pairs per launch
+    # batch g of slot j of this rank: the pairs of make_inputs "rank" (rank * S + j) * G + g
+    # (distinct pairs per batch, slot and rank, cycled through the 20 ordered pairs of the 5 frames)
+    slot_inputs = [make_group_inputs(B, G, (rank * S + j) * G, device) for j in range(S)]
     sel, levels_nchw, K = slot_inputs[0]
 
     def packed(levels):
@@ -244,13 +263,13 @@ def main():
 
     levels = packed(levels_nchw) if a.layout == "c4" else levels_nchw
     # R [B,3,3] and t [B,3] as two contiguous views of one buffer: one reset copy per step
-    pose_init = torch.cat((torch.eye(3, device=device).repeat(B, 1, 1).reshape(-1), torch.zeros(B * 3, device=device)))
+    pose_init = torch.cat((torch.eye(3, device=device).repeat(BG, 1, 1).reshape(-1), torch.zeros(BG * 3, device=device)))
 
     def make_step(levels, K=K):
-        solver = ic.PyramidSolver(levels, K, iters=ITERS, remove_tru_sigma=True,
+        solver = ic.PyramidSolver(levels, K, iters=ITERS, remove_tru_sigma=True, group=B,
                                   schedule=os.environ.get("DPFT_BENCH_SCHEDULE"))  # A/B only
         pose = pose_init.clone()
-        R, t = pose[:9 * B].view(B, 3, 3), pose[9 * B:].view(B, 3)
+        R, t = pose[:9 * BG].view(BG, 3, 3), pose[9 * BG:].view(BG, 3)
 
         def solve():
             pose.copy_(pose_init)
@@ -291,7 +310,7 @@ def main():
     # N > 1: the pose gather of step k runs on the collective stream while step k + 1
     # solves (double-buffered output; poses packed into a fresh buffer first, on the
     # slot's stream); every gather is waited for inside the timed region (drain())
-    gathered = [torch.empty(world * B, 12, device=device) for _ in range(2)] if world > 1 else None
+    gathered = [torch.empty(world * BG, 12, device=device) for _ in range(2)] if world > 1 else None
     pending = [None]
     nstep = [0]
 
@@ -349,7 +368,7 @@ def main():
     for sl in slots:
         ic.check_status(sl[0].status)
     ms_per_step = elapsed / a.steps * 1e3
-    iters_total = world * B * LEVELS * ITERS * a.steps
+    iters_total = world * BG * LEVELS * ITERS * a.steps
     value = iters_total / elapsed
     # latency of one solve (slot 0 alone, back to back on one stream), rank 0 only
     latency_ms = None
@@ -383,7 +402,7 @@ def main():
     kern_us = ev0.elapsed_time(ev1) / (groups * len(l0_group)) * 1e3
     alg_bytes = solver.algorithmic_bytes(0)
     achieved = alg_bytes / (kern_us * 1e-6) / 1e9
-    traffic = l0_traffic() if a.layout == "c4" and B == 8 else None
+    traffic = l0_traffic(BG, B) if a.layout == "c4" else None
     copy_gbs = copy_peak_gbs(device) if rank == 0 else None
     read_gbs = read_peak_gbs(device, alg_bytes) if rank == 0 else None
 
@@ -403,7 +422,7 @@ def main():
         o_el = time.perf_counter() - tt0
         dpose = max((o_R - R).abs().max().item(), (o_t - t).abs().max().item())
         other = {"layout": other_layout, "ms_per_step": o_el / a.steps * 1e3,
-                 "value": B * LEVELS * ITERS * a.steps / o_el, "max_abs_pose_diff_vs_headline": dpose,
+                 "value": BG * LEVELS * ITERS * a.steps / o_el, "max_abs_pose_diff_vs_headline": dpose,
                  "pack_us_all_levels_both_frames": pack_time_us(levels_nchw)}
         del o_solver
 
@@ -426,13 +445,14 @@ def main():
             "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "f32",
             "data": "synthetic: deterministic triangle-wave features of the 5 TUM fr1/desk example frames",
             "config": {"workload": "cfg2/cfg3 shard: 640x480, C=32, Cs=1, 4 levels x 3 GN iters, "
-                                   "remove_tru_sigma, B pairs per GPU", "pairs_per_gpu": B,
+                                   "remove_tru_sigma, batches of B pairs per GPU", "pairs_per_gpu": B,
                        "global_batch": world * B, "parallelism": f"pair-sharded x{world}, RCCL all-gather of poses",
-                       "graph": graphed, "feature_layout": a.layout, "inflight": S,
+                       "graph": graphed, "feature_layout": a.layout,
+                       "batches_per_launch": G, "pairs_per_launch": BG, "inflight": S,
                        "setup_warm_ms": a.setup_warm_ms},
             "latency_ms_per_solve": latency_ms,
-            "pairs_per_s": world * B * a.steps / elapsed,
-            "l0_iters_per_s": world * B * ITERS * a.steps / elapsed,
+            "pairs_per_s": world * BG * a.steps / elapsed,
+            "l0_iters_per_s": world * BG * ITERS * a.steps / elapsed,
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": achieved / HBM_PEAK_GBS,
                          "traffic": traffic["hbm_bytes"] if traffic else None,

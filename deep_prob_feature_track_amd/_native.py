@@ -21,6 +21,8 @@ FEATURES_C4 = 0x8
 SCHEDULES = {"auto": 0x00, "march": 0x10, "split": 0x20}  # DPFT_SCHED_*
 EXT_SLOT_SHIFT = 12       # DPFT_EXT_SLOT(k) = (k + 1) << 12
 EXTREMA_READY = 0x10000
+GROUP_SHIFT = 20          # DPFT_GROUP(n) = n << 20: n pairs per independent batch (bits 20-27)
+GROUP_MAX_BATCHES = 32
 STATUS_NONFINITE = 0x1
 ABI_VERSION = 2
 

@@ -206,7 +206,14 @@ static_assert(kMMGrid <= kMaxMMBlocks, "minmax partials");
 static_assert(DPFT_MARCH_SKEW >= 0 && DPFT_MARCH_SKEW < 64, "band skew in 64ths");
 constexpr int kMaxPairs = 2048;  // per call (one completion counter per pair)
 constexpr int kMaxGrid = 4096;   // reduce-kernel workgroups (resident capacity is far below)
-constexpr size_t kCtrlBytes = 16384;
+// Independent batches in one call (DPFT_GROUP): per batch a completion counter of the
+// batch solve (kCtlGDone + g), sigma0 extrema per (slot, batch) (kCtlGExt; slot index
+// kMaxExtSlots = a call without DPFT_EXT_SLOT) and the pre-pass counters per (level, batch).
+constexpr int kMaxGroups = 32;
+constexpr int kCtlGDone = 32, kCtlGExt = 4096, kCtlGMMDone = kCtlGExt + 2 * (kMaxExtSlots + 1) * kMaxGroups;
+constexpr size_t kCtrlBytes = 20480;
+static_assert(kCtlGDone + kMaxGroups <= kCtlPart, "batch counters");
+static_assert((kCtlGMMDone + 4 * kMaxGroups) * 4 <= kCtrlBytes, "ctrl area (batches)");
 static_assert((kCtlPart + 2 * kMaxMMBlocks) * 4 <= kCtlPair * 4, "ctrl area");
 static_assert((kCtlPair + kMaxPairs) * 4 <= kCtrlBytes, "ctrl area");
 static_assert(kCtlTail >= kCtlPair + kMaxPairs && (kCtlTail + kTailWG + 2 * kTailPairs + 2) * 4 <= kCtrlBytes, "tail stamps");
@@ -283,6 +290,25 @@ __device__ __forceinline__ int xcd_remap(int orig, int n) {
   const int xcd = orig & 7, q = n >> 3, r = n & 7;
   const int base = xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q;
   return base + (orig >> 3);
+}
+
+// ic_reduce_kernel: blockIdx -> (pair-major) workgroup slot.  xcd_remap keeps a pair's
+// workgroups on one XCD; with several pairs per XCD (B > 8 at the resident grid) the
+// workgroups of each pair are also taken half from the XCD's first dispatch round (the
+// first workgroup on each CU, favoured by the oldest-first issue arbitration) and half
+// from the second, as with one pair per XCD -- the band skew assumes exactly that split.
+// Without it the second pair of an XCD ran entirely as second workgroups and finished
+// last (B = 16: 313 us per level-0 launch, 156 us per 8 pairs against 141 at B = 8).
+__device__ __forceinline__ int pair_slot_remap(int orig, int n, int nbpp) {
+  int kb = xcd_remap(orig, n);
+  const int q = n >> 3;
+  if ((n & 7) == 0 && (nbpp & 1) == 0 && q % nbpp == 0 && q / nbpp >= 2 && (q & 1) == 0) {
+    const int xb = kb - kb % q, i = kb - xb, h = q >> 1, hp = nbpp >> 1;
+    const bool second = i >= h;
+    const int ii = second ? i - h : i, pin = ii / hp;
+    kb = xb + pin * nbpp + (ii - pin * hp) + (second ? hp : 0);
+  }
+  return kb;
 }
 
 struct Taps {
@@ -385,7 +411,8 @@ struct FinParams {
   int nbpp, B;        // reduce kernel: workgroups (records) per pair, pairs
   double* prec;       // [B][kPRec] per-pair records
   uint32_t* pair_cnt; // [B] completion counters
-  uint32_t* done_cnt; // pairs finished
+  uint32_t* done_cnt; // pairs finished (one counter per independent batch)
+  int group;          // pairs per independent batch (B: the call is one batch)
   int nblocks, per_pair, HW;
   uint32_t flags;
   int no_update;      // DPFT_ITER_NO_UPDATE: normal equations out, pose unchanged
@@ -970,6 +997,24 @@ __device__ void finalize_batch(const FinParams& q) {
   finalize_batch_from(q, [&](int, int i) { return r[i]; });
 }
 
+// Called by the workgroup that reduced pair b: the last of pair b's batch to finish
+// (DPFT_GROUP: q.group pairs per independent batch, else the whole call) solves that
+// batch -- its own truncated-sigma extrema, as if it had been a call of its own.
+__device__ bool finalize_group(const FinParams& q, int b) {
+  const int g = b / q.group, b0 = g * q.group;
+  if (!block_is_last(q.done_cnt + g, 1u, (uint32_t)q.group)) return false;
+  FinParams qg = q;
+  qg.B = q.group;
+  qg.prec = q.prec + (size_t)b0 * kPRec;
+  qg.R = q.R ? q.R + 9 * b0 : nullptr;
+  qg.t = q.t ? q.t + 3 * b0 : nullptr;
+  qg.jtj_out = q.jtj_out ? q.jtj_out + 36 * b0 : nullptr;
+  qg.jtr_out = q.jtr_out ? q.jtr_out + 6 * b0 : nullptr;
+  qg.invalid_out = q.invalid_out ? q.invalid_out + b0 : nullptr;
+  finalize_batch(qg);
+  return true;
+}
+
 // Wave min / max trees (fixed order), every value moved before each step's wait.
 // v[0], v[1]: min; v[2], v[3]: max
 __device__ __forceinline__ void wave_minmax4(float (&v)[4]) {
@@ -1172,11 +1217,12 @@ __global__ __launch_bounds__(kThreads, DPFT_MIN_WAVES) void ic_reduce_kernel(Ite
 
   const int tid = threadIdx.x, lane = tid & 63, wave = wave_id();
   const int W = p.W, H = p.H, HW = H * W;
-  const int kb = xcd_remap(blockIdx.x, gridDim.x);
+  const int kb = pair_slot_remap(blockIdx.x, gridDim.x, p.nbpp);
   const int b = kb / p.nbpp, jb = kb - b * p.nbpp;
   const int seg_begin = b * p.per_pair + (int)(((long)p.per_pair * jb) / p.nbpp);
   const int seg_end = b * p.per_pair + (int)(((long)p.per_pair * (jb + 1)) / p.nbpp);
-  const float g0min = TRU ? dec_ord(p.ext[0]) : 0.f, g0max = TRU ? dec_ord(p.ext[1]) : 0.f;
+  const int grp2 = 2 * (b / p.fin.group);  // this pair's batch: its sigma0 extrema
+  const float g0min = TRU ? dec_ord(p.ext[grp2]) : 0.f, g0max = TRU ? dec_ord(p.ext[grp2 + 1]) : 0.f;
   const uint32_t planeB = (uint32_t)HW * 4u;
   const int nch = C4 ? C / 4 : (C + kCK - 1) / kCK;    // one unit = one channel quad / kCK channels
   const int nunits = (nch + kRing - 1) / kRing * kRing;  // units per step, padded to the ring (empty tail units)
@@ -2053,19 +2099,17 @@ __global__ __launch_bounds__(kThreads, DPFT_MIN_WAVES) void ic_reduce_kernel(Ite
       st_ag(p.ctrl + kCtlTail + kTailWG + 2 * b + 1, (uint32_t)wall_clock64());
     }
 #endif
-    if (block_is_last(p.fin.done_cnt, 1u, (uint32_t)p.B)) {
 #if DPFT_TAIL_PROF
-      const uint32_t t19 = (uint32_t)wall_clock64();
+    const uint32_t t19 = (uint32_t)wall_clock64();  // (before the batch-last handshake)
 #endif
-      finalize_batch(p.fin);
+    [[maybe_unused]] const bool solved = finalize_group(p.fin, b);
 #if DPFT_TAIL_PROF
-      __syncthreads();
-      if (threadIdx.x == 0) {
-        st_ag(p.ctrl + kCtlTail + kTailWG + 2 * kTailPairs, t19);
-        st_ag(p.ctrl + kCtlTail + kTailWG + 2 * kTailPairs + 1, (uint32_t)wall_clock64());
-      }
-#endif
+    __syncthreads();
+    if (threadIdx.x == 0 && solved) {
+      st_ag(p.ctrl + kCtlTail + kTailWG + 2 * kTailPairs, t19);
+      st_ag(p.ctrl + kCtlTail + kTailWG + 2 * kTailPairs + 1, (uint32_t)wall_clock64());
     }
+#endif
   }
 }
 
@@ -2214,7 +2258,7 @@ __global__ __launch_bounds__(kThreads) void finalize_kernel(FinParams q) {
 #endif
   __shared__ float sc[kFinScratch];
   pair_reduce2(q, blockIdx.x, sc);
-  if (block_is_last(q.done_cnt, 1u, (uint32_t)q.B)) finalize_batch(q);
+  finalize_group(q, blockIdx.x);
 }
 
 // ============================================================ channel-split reduce kernel (coarse levels)
@@ -2237,7 +2281,8 @@ __device__ __forceinline__ void split_pass(const IterParams& p, int b, int jb, i
   const int lane = threadIdx.x & 63, wave = wave_id();
   const int W = p.W, H = p.H, HW = H * W;
   const int U = p.tiles_x * H;
-  const float g0min = TRU ? dec_ord(p.ext[0]) : 0.f, g0max = TRU ? dec_ord(p.ext[1]) : 0.f;
+  const int grp2 = 2 * (b / p.fin.group);  // this pair's batch: its sigma0 extrema
+  const float g0min = TRU ? dec_ord(p.ext[grp2]) : 0.f, g0max = TRU ? dec_ord(p.ext[grp2 + 1]) : 0.f;
   const uint32_t planeB = (uint32_t)HW * 4u;
   const float fx = p.K[4 * b + 0], fy = p.K[4 * b + 1], cx = p.K[4 * b + 2], cy = p.K[4 * b + 3];
   float Rm[9], tv[3];
@@ -2395,7 +2440,7 @@ __global__ __launch_bounds__(kThreads, 4) void ic_split_kernel(IterParams p) {  
 
   if (!kSplitSepFin && p.fin_on && block_is_last(p.fin.pair_cnt + b, 1u, (uint32_t)p.nbpp)) {
     pair_reduce2(p.fin, b, &qs[0][0][0][0]);  // LDS scratch: the channel-sum buffers
-    if (block_is_last(p.fin.done_cnt, 1u, (uint32_t)p.B)) finalize_batch(p.fin);
+    finalize_group(p.fin, b);
   }
 }
 
@@ -2676,15 +2721,19 @@ __global__ __launch_bounds__(kThreads) void minmax_kernel(const float* __restric
 
 // Every level's sigma0 extrema in one launch (blockIdx.y = level): one pose-independent
 // pre-pass per pyramid solve instead of one launch per level.
+// DPFT_GROUP: blockIdx.y = level * groups + batch, each batch's extrema over its own
+// pairs into its own slot word pair (one call = one batch: exactly the per-level pass).
 struct MMLevels {
   const float* s[4];
-  size_t n[4];
+  size_t n[4];  // floats per batch
   int slot[4];
+  int groups;
 };
 __global__ __launch_bounds__(kThreads) void minmax_levels_kernel(MMLevels a, uint32_t* ctrl) {
-  const int l = blockIdx.y;
-  minmax_body(a.s[l], a.n[l], ctrl, a.slot[l], reinterpret_cast<float*>(ctrl + kCtlPart) + 2 * l * gridDim.x,
-              ctrl + kCtlMMDoneL + l);
+  const int l = blockIdx.y / a.groups, g = blockIdx.y - l * a.groups;
+  minmax_body(a.s[l] + (size_t)g * a.n[l], a.n[l], ctrl, a.slot[l] + 2 * g,
+              reinterpret_cast<float*>(ctrl + kCtlPart) + 2 * blockIdx.y * gridDim.x,
+              ctrl + (a.groups > 1 ? kCtlGMMDone : kCtlMMDoneL) + blockIdx.y);
 }
 
 // ============================================================ depth preprocessing
@@ -2812,7 +2861,26 @@ int check_desc(const DpftLevelDesc* d) {
     return fail(DPFT_E_INVALID, "NO_UNCERTAINTY (IC tracker) excludes REMOVE_TRU_SIGMA and COMBINE_ICP");
   if ((d->flags & DPFT_FEATURES_C4) && (d->C % 4 != 0 || (d->Cs != 1 && !(d->flags & DPFT_NO_UNCERTAINTY))))
     return fail(DPFT_E_INVALID, "FEATURES_C4 needs C %% 4 == 0 and one sigma plane (C=%d, Cs=%d)", d->C, d->Cs);
+  const int gs = (int)((d->flags & DPFT_GROUP_MASK) >> DPFT_GROUP_SHIFT);
+  if (gs != 0 && gs < d->B) {
+    if (d->B % gs != 0 || d->B / gs > kMaxGroups)
+      return fail(DPFT_E_INVALID, "DPFT_GROUP(%d): B=%d must be a multiple of it, at most %d batches", gs, d->B,
+                  kMaxGroups);
+    if (d->flags & DPFT_COMBINE_ICP) return fail(DPFT_E_INVALID, "DPFT_GROUP: not with COMBINE_ICP");
+  }
   return DPFT_OK;
+}
+
+// pairs per independent batch of the call (DPFT_GROUP; B = one batch)
+int group_of(const DpftLevelDesc& d) {
+  const int gs = (int)((d.flags & DPFT_GROUP_MASK) >> DPFT_GROUP_SHIFT);
+  return (gs == 0 || gs >= d.B) ? d.B : gs;
+}
+// ctrl word of batch 0's sigma0 extrema for this call (batch g: + 2 g)
+int ext_word(const DpftLevelDesc& d) {
+  const int xslot = (int)((d.flags & DPFT_EXT_SLOT_MASK) >> DPFT_EXT_SLOT_SHIFT);  // 0: none
+  if (group_of(d) == d.B) return xslot ? kCtlExtSlots + 2 * (xslot - 1) : kCtlMin;
+  return kCtlGExt + 2 * kMaxGroups * (xslot ? xslot - 1 : kMaxExtSlots);
 }
 
 int check_tensors(const DpftLevelTensors* t, uint32_t flags = 0) {
@@ -2886,8 +2954,7 @@ IterParams make_params(const DpftLevelDesc& d, const DpftLevelTensors& tt, const
   p.nblocks = g.nblocks;
   p.flags = d.flags;
   p.ctrl = reinterpret_cast<uint32_t*>(ws);
-  const int xslot = (int)((d.flags & DPFT_EXT_SLOT_MASK) >> DPFT_EXT_SLOT_SHIFT);  // 0: none
-  p.ext = p.ctrl + (xslot ? kCtlExtSlots + 2 * (xslot - 1) : kCtlMin);
+  p.ext = p.ctrl + ext_word(d);
   p.rec = reinterpret_cast<float*>(static_cast<char*>(ws) + rec_offset(d));
   // rows per step of the reduce kernel (4 waves x rows per lane of the instantiation launched)
   p.rps = 4 * ((d.flags & DPFT_FEATURES_C4) ? kRPL4 : (d.Cs == 1 || (d.flags & DPFT_NO_UNCERTAINTY)) ? kRPL : 1);
@@ -2906,7 +2973,8 @@ IterParams make_params(const DpftLevelDesc& d, const DpftLevelTensors& tt, const
   p.fin.rec = p.rec;
   p.fin.prec = reinterpret_cast<double*>(static_cast<char*>(ws) + kCtrlBytes);
   p.fin.pair_cnt = p.ctrl + kCtlPair;
-  p.fin.done_cnt = p.ctrl + kCtlDone;
+  p.fin.group = group_of(d);
+  p.fin.done_cnt = p.ctrl + (p.fin.group < d.B ? kCtlGDone : kCtlDone);
   p.fin.nblocks = g.nblocks;
   p.fin.per_pair = g.per_pair;
   p.fin.HW = d.H * d.W;
@@ -2934,10 +3002,10 @@ int launch_minmax(const DpftLevelDesc& d, const DpftLevelTensors& tt, void* ws, 
   uint32_t* ctrl = reinterpret_cast<uint32_t*>(ws);
   int rc;
   if ((d.flags & DPFT_REMOVE_TRU_SIGMA) && !(d.flags & DPFT_EXTREMA_READY)) {
-    const int xslot = (int)((d.flags & DPFT_EXT_SLOT_MASK) >> DPFT_EXT_SLOT_SHIFT);
-    if ((rc = minmax_into(tt.s0, (size_t)d.B * d.Cs * d.H * d.W, ctrl, xslot ? kCtlExtSlots + 2 * (xslot - 1) : kCtlMin,
-                          st)))
-      return rc;
+    const int gs = group_of(d);  // one pass per independent batch (DPFT_GROUP)
+    const size_t n = (size_t)gs * d.Cs * d.H * d.W;
+    for (int g = 0; g < d.B / gs; ++g)
+      if ((rc = minmax_into(tt.s0 + g * n, n, ctrl, ext_word(d) + 2 * g, st))) return rc;
   }
   if (d.flags & DPFT_COMBINE_ICP) {
     const size_t n = (size_t)d.B * d.H * d.W;
@@ -3143,6 +3211,7 @@ int residual_impl(const DpftLevelDesc* desc, const DpftLevelTensors* tt, int P, 
   if ((rc = check_tensors(tt, desc->flags))) return rc;
   if (!R || !t || !loss || !ws) return fail(DPFT_E_INVALID, "null pose / loss / workspace");
   if (P < 1 || P > kMaxPairs) return fail(DPFT_E_INVALID, "n_poses=%d outside [1, %d]", P, kMaxPairs);
+  if (group_of(*desc) < desc->B) return fail(DPFT_E_INVALID, "DPFT_GROUP: solver entry points only");
   if (ws_bytes < ws_need_poses(*desc, P))
     return fail(DPFT_E_WORKSPACE, "workspace %zu < %zu", ws_bytes, ws_need_poses(*desc, P));
   const Geometry g = plan(*desc);
@@ -3261,6 +3330,7 @@ int sigma_extrema_impl(const DpftLevelDesc* descs, const DpftLevelTensors* tenso
   if (!descs || !tensors || !workspace) return fail(DPFT_E_INVALID, "null pointer");
   if (levels < 1 || levels > 4) return fail(DPFT_E_INVALID, "levels=%d outside [1, 4]", levels);
   MMLevels a;
+  a.groups = 1;
   size_t nmax = 0;
   for (int l = 0; l < 4; ++l) {
     a.s[l] = nullptr;
@@ -3275,14 +3345,18 @@ int sigma_extrema_impl(const DpftLevelDesc* descs, const DpftLevelTensors* tenso
     if (!xslot) return fail(DPFT_E_INVALID, "level %d has no extrema slot (DPFT_EXT_SLOT)", l);
     if (!tensors[l].s0) return fail(DPFT_E_INVALID, "level %d: null sigma0", l);
     if (workspace_bytes < ws_need(d)) return fail(DPFT_E_WORKSPACE, "workspace %zu < %zu", workspace_bytes, ws_need(d));
+    if (l == 0) a.groups = d.B / group_of(d);
+    if (d.B / group_of(d) != a.groups) return fail(DPFT_E_INVALID, "level %d: another DPFT_GROUP than level 0", l);
     a.s[l] = tensors[l].s0;
-    a.n[l] = (size_t)d.B * d.Cs * d.H * d.W;
-    a.slot[l] = kCtlExtSlots + 2 * (xslot - 1);
+    a.n[l] = (size_t)group_of(d) * d.Cs * d.H * d.W;  // per batch
+    a.slot[l] = ext_word(d);
     nmax = std::max(nmax, a.n[l]);
   }
-  const int grid = (int)std::min<size_t>((nmax + kThreads * 16 - 1) / (kThreads * 16), kMMGrid);
+  // partial extrema: 2 words per workgroup and (level, batch), kMaxMMBlocks pairs in all
+  const int grid = (int)std::max<size_t>(1, std::min<size_t>(std::min<size_t>((nmax + kThreads * 16 - 1) / (kThreads * 16), kMMGrid),
+                                                              (size_t)kMaxMMBlocks / ((size_t)levels * a.groups)));
   static_assert(4 * 2 * kMMGrid <= 2 * kMaxMMBlocks, "per-level minmax partials");
-  hipLaunchKernelGGL(minmax_levels_kernel, dim3(grid, levels), dim3(kThreads), 0, st, a,
+  hipLaunchKernelGGL(minmax_levels_kernel, dim3(grid, levels * a.groups), dim3(kThreads), 0, st, a,
                      static_cast<uint32_t*>(workspace));
   return hip_check("minmax_levels_kernel");
 }

@@ -493,7 +493,11 @@ class PyramidSolver:
     """
 
     def __init__(self, levels, K, iters=3, remove_tru_sigma=False, combine_icp=False, icp_weight=0.01,
-                 schedule=None):
+                 schedule=None, group=None):
+        """group: pairs per independent batch (DPFT_GROUP).  The B pairs are then B / group
+        consecutive batches, each solved exactly as its own call -- its own batch-global
+        truncated-sigma extrema -- in launches that cover all of them (fewer, larger
+        launches); None = one batch."""
         dev = levels[0]["x0"].device
         self.status = torch.zeros(1, dtype=torch.int32, device=dev)
         self.calls = []
@@ -507,6 +511,15 @@ class PyramidSolver:
         # sigma): each level keeps them in its own workspace slot and skips the
         # per-level min/max launch (dpft_sigma_extrema_levels, DPFT_EXTREMA_READY).
         # Not with combine_icp (its depth1 pass shares the min/max scratch words).
+        B = self.calls[0].B
+        if group is not None and group < B:
+            if group < 1 or B % group or B // group > N.GROUP_MAX_BATCHES or group >= 256:
+                raise ValueError(f"group={group}: B={B} must be a multiple, at most {N.GROUP_MAX_BATCHES} batches")
+            if combine_icp:
+                raise ValueError("group: not with combine_icp (its depth extrema are per call)")
+            for c in self.calls:
+                c.desc.flags |= group << N.GROUP_SHIFT
+        self.group = group if group is not None and group < B else B
         self.remove_tru_sigma = bool(remove_tru_sigma)
         self.extrema_prepass = bool(remove_tru_sigma) and not combine_icp and len(self.calls) <= 4
         if self.extrema_prepass:

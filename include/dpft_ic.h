@@ -85,6 +85,17 @@ extern "C" {
 #define DPFT_EXT_SLOT(k)    ((((uint32_t)(k)) + 1u) << DPFT_EXT_SLOT_SHIFT)
 #define DPFT_EXTREMA_READY  0x10000u
 
+/* Independent batches in one call (bits 20-27): DPFT_GROUP(n) splits the B pairs into
+ * B / n consecutive batches of n pairs (B % n == 0, at most 32 batches), each solved
+ * exactly as a call of its own -- its own batch-global truncated-sigma extrema
+ * (algorithms.py:1975-1980) and sigma0 pre-pass -- while every launch covers all B
+ * pairs (fewer, larger launches: the per-launch ramp, finish spread and finalize are
+ * paid once for all batches).  0 (or n >= B): the call is one batch.  Solver entry
+ * points only (not with COMBINE_ICP; the residual entry points reject it).          */
+#define DPFT_GROUP_SHIFT 20
+#define DPFT_GROUP_MASK  0x0FF00000u
+#define DPFT_GROUP(n)    ((((uint32_t)(n)) << DPFT_GROUP_SHIFT) & DPFT_GROUP_MASK)
+
 /* device status word bits */
 #define DPFT_STATUS_NONFINITE 0x1u /* a JtJ / JtR reduction was not finite         */
 

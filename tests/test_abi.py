@@ -33,3 +33,21 @@ def test_invalid_descriptor_is_rejected_without_device_work():
     assert rc == -1 and b"bad shape" in L.dpft_last_error()
     cs = N.LevelDesc(1, 8, 3, 120, 160, 3, 0, 0.0)  # Cs must be 1 or C
     assert L.dpft_workspace_size(ctypes.byref(cs)) == 0
+
+
+def test_group_descriptor_validation_without_device_work():
+    """DPFT_GROUP(n): B a multiple of n, at most 32 batches, not with COMBINE_ICP; n >= B
+    (or 0) is one batch.  Checked by the descriptor validation every entry point runs."""
+    import ctypes
+    L = N.lib()
+    G = lambda n: n << N.GROUP_SHIFT
+
+    def ws(B, flags):
+        return L.dpft_workspace_size(ctypes.byref(N.LevelDesc(B, 32, 1, 480, 640, 3, flags, 0.01)))
+    base = N.REMOVE_TRU_SIGMA | N.FEATURES_C4
+    assert ws(32, base | G(8)) > 0 and ws(32, base | G(8)) == ws(32, base)  # same workspace
+    assert ws(8, base | G(8)) > 0 and ws(8, base | G(16)) > 0             # one batch
+    assert ws(12, base | G(8)) == 0                                        # not a multiple
+    assert b"DPFT_GROUP" in L.dpft_last_error()
+    assert ws(64, base | G(1)) == 0                                        # 64 batches > 32
+    assert ws(32, N.REMOVE_TRU_SIGMA | N.COMBINE_ICP | G(8)) == 0          # ICP: per-call depth extrema

@@ -434,3 +434,106 @@ def test_inflight_solves_bit_identical():
             ic.check_status(solvers[j].status)
             assert torch.equal(poses[j][0], alone[j][0]) and torch.equal(poses[j][1], alone[j][1])
     assert not torch.equal(alone[0][1], alone[1][1])
+
+
+def _grouped_case(dev, G=4, B=8):
+    """G batches of B copies of the golden cfg2 pair; batch g's sigma0 / sigma1 scaled by
+    1 + g / 4 (so every batch has its own sigma extrema) and each pair started from its
+    own initial translation."""
+    from deep_prob_feature_track_amd import ic
+    case, z = golden_io.load("cfg2_640x480_c32")
+    lv = golden_io.levels_torch(case, torch.float32, dev)
+    R0, t0 = golden_io.init_pose(case, torch.float32, dev)
+    K = torch.from_numpy(case["K"]).to(dev)
+    n = G * B
+    rep = lambda x: x.repeat(n, *([1] * (x.dim() - 1)))
+    scale = (1.0 + torch.arange(G, device=dev, dtype=torch.float32) / 4).repeat_interleave(B).view(n, 1, 1, 1)
+    levels = [dict(x0=rep(ic.pack_features(d["f0"])), x1=rep(ic.pack_features(d["f1"])), invD0=rep(d["invD0"]),
+                   invD1=rep(d["invD1"]), sigma0=(rep(d["s0"]) * scale).contiguous(),
+                   sigma1=(rep(d["s1"]) * scale).contiguous()) for d in lv]
+    t = rep(t0.reshape(-1, 3)).clone()
+    t[:, 0] += 2e-3 * (torch.arange(n, device=dev, dtype=torch.float32) % B) / B
+    return z, levels, rep(K), rep(R0).contiguous(), t.contiguous()
+
+
+def _invalid_counts(solver, level, R, t):
+    """#invalid pixels per pair of one no-update iteration of `level` (exact integers)."""
+    import ctypes
+    from deep_prob_feature_track_amd import ic
+    c = solver.calls[level]
+    inv = torch.zeros(c.B, dtype=torch.int32, device=R.device)
+    Rc, tc = R.contiguous().clone(), t.contiguous().clone()  # kept alive across the launch
+    solver.prepare_extrema()
+    rc = ic.N.lib().dpft_ic_iterate(ctypes.byref(c.desc), ctypes.byref(c.tens), ic._ptr(Rc), ic._ptr(tc), None,
+                                    None, ic._ptr(inv), 1 | 4, ic._ptr(solver.ws), solver.ws_bytes,
+                                    ic._stream(R.device))
+    ic.N.check(rc, "dpft_ic_iterate")
+    torch.cuda.synchronize()
+    return inv.cpu().numpy()
+
+
+@pytest.mark.gpu
+def test_grouped_batches_solve_as_separate_calls():
+    """DPFT_GROUP (bench.py --groups): 4 independent 8-pair batches in every launch.  Each
+    batch is solved as a call of its own -- its own truncated-sigma extrema: the invalid
+    pixel counts equal those of separate 8-pair calls exactly (and differ from one
+    32-pair batch, whose extrema span all four), the poses within the fp32 summation
+    noise (the launch splits each pair into fewer workgroup records), and batch 0 (the
+    golden pair, unscaled) lands on the reference's poses."""
+    from deep_prob_feature_track_amd import ic
+    dev = _dev()
+    G, B = 4, 8
+    z, levels, K, R0, t0 = _grouped_case(dev, G, B)
+    grouped = ic.PyramidSolver(levels, K, iters=3, remove_tru_sigma=True, group=B)
+    assert grouped.group == B
+    R, t = R0.clone(), t0.clone()
+    grouped.run(R, t)
+    torch.cuda.synchronize()
+    ic.check_status(grouped.status)
+    sl = lambda g: slice(g * B, (g + 1) * B)
+    for g in range(G):
+        lv_g = [{k: v[sl(g)] for k, v in d.items()} for d in levels]
+        alone = ic.PyramidSolver(lv_g, K[sl(g)].contiguous(), iters=3, remove_tru_sigma=True)
+        Ra, ta = R0[sl(g)].clone(), t0[sl(g)].clone()
+        alone.run(Ra, ta)
+        torch.cuda.synchronize()
+        # (another fp32 summation grouping: measured up to 2.6e-5 on t; the reference's own
+        # fp32 noise floor at 640x480 is 9.7e-5)
+        torch.testing.assert_close(R[sl(g)], Ra, rtol=0, atol=5e-5)
+        torch.testing.assert_close(t[sl(g)], ta, rtol=0, atol=5e-5)
+        for level in (0, 2):  # marching and split schedules
+            assert np.array_equal(_invalid_counts(grouped, level, R, t)[sl(g)],
+                                  _invalid_counts(alone, level, R[sl(g)], t[sl(g)]))
+    one_batch = ic.PyramidSolver(levels, K, iters=3, remove_tru_sigma=True)
+    assert not np.array_equal(_invalid_counts(one_batch, 0, R, t), _invalid_counts(grouped, 0, R, t))
+    for prec in ("f32", "f64"):
+        assert np.abs(R[sl(0)].cpu().numpy()[:1] - z[f"{prec}_R"][-1]).max() <= SE3_TOL
+
+
+@pytest.mark.gpu
+def test_grouped_solve_deterministic_and_graph_capturable():
+    """The grouped solve replayed from one HIP graph equals the eager solve bit for bit
+    (fixed-order reductions, per-batch completion counters left at zero)."""
+    from deep_prob_feature_track_amd import ic
+    dev = _dev()
+    z, levels, K, R0, t0 = _grouped_case(dev, 2, 8)
+    solver = ic.PyramidSolver(levels, K, iters=3, remove_tru_sigma=True, group=8)
+    R, t = R0.clone(), t0.clone()
+    solver.run(R, t)
+    torch.cuda.synchronize()
+    Re, te = R.clone(), t.clone()
+    s = torch.cuda.Stream(dev)
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.stream(s):
+        R.copy_(R0)
+        t.copy_(t0)
+        solver.run(R, t)
+    torch.cuda.synchronize()
+    with torch.cuda.graph(g):
+        R.copy_(R0)
+        t.copy_(t0)
+        solver.run(R, t)
+    for _ in range(3):
+        g.replay()
+        torch.cuda.synchronize()
+        assert torch.equal(R, Re) and torch.equal(t, te)

@@ -15,6 +15,7 @@ from deep_prob_feature_track_amd import ic
 p = argparse.ArgumentParser()
 p.add_argument("--level", type=int, default=0)
 p.add_argument("--batch", type=int, default=8)
+p.add_argument("--groups", type=int, default=1, help="independent --batch-pair batches per launch (DPFT_GROUP)")
 p.add_argument("--reps", type=int, default=20)
 p.add_argument("--mode", choices=["reduce", "iterate", "level"], default="reduce",
                help="level: the solve's launches at one level (iterations forward, reverse, forward)")
@@ -26,13 +27,13 @@ p.add_argument("--from-solve", action="store_true",
                help="start from the poses of one full pyramid solve (the bench's operating point) instead of identity")
 a = p.parse_args()
 dev = torch.device("cuda:0")
-sel, levels, K = bench.make_inputs(a.batch, 0, dev)
+sel, levels, K = bench.make_group_inputs(a.batch, a.groups, 0, dev)
 if a.c4:
     for d in levels:
         d["x0"], d["x1"] = ic.pack_features(d["x0"]), ic.pack_features(d["x1"])
-solver = ic.PyramidSolver(levels, K, iters=3, remove_tru_sigma=True, schedule=a.schedule)
-R = torch.eye(3, device=dev).repeat(a.batch, 1, 1).contiguous()
-t = torch.zeros(a.batch, 3, device=dev)
+solver = ic.PyramidSolver(levels, K, iters=3, remove_tru_sigma=True, schedule=a.schedule, group=a.batch)
+R = torch.eye(3, device=dev).repeat(a.batch * a.groups, 1, 1).contiguous()
+t = torch.zeros(a.batch * a.groups, 3, device=dev)
 import ctypes
 from deep_prob_feature_track_amd import _native as N
 if a.from_solve:
@@ -89,5 +90,5 @@ for level in ([a.level] if a.level >= 0 else range(len(solver.calls))):
             x = f[b * per:(b + 1) * per]
             print("   pair %d: finish min %.1f  median %.1f  max %.1f | pair-last detected %.1f, pair reduced %.1f"
                   % (b, x.min(), np.median(x), x.max(), pr[b, 0], pr[b, 1]))
-    print(f"{os.path.basename(os.environ.get('DPFT_LIB', 'libdpft_ic.so'))}{' c4' if a.c4 else ''}{' ' + a.schedule if a.schedule else ''} {a.mode} level {level} B={a.batch}: "
+    print(f"{os.path.basename(os.environ.get('DPFT_LIB', 'libdpft_ic.so'))}{' c4' if a.c4 else ''}{' ' + a.schedule if a.schedule else ''} {a.mode} level {level} B={a.batch}x{a.groups}: "
           f"{us:.1f} us/launch, {gbs:.0f} GB/s algorithmic ({gbs / 80:.1f}% of 8 TB/s)", flush=True)

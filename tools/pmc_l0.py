@@ -40,10 +40,10 @@ def isa_sha():
     return (B.isa_hashes(os.path.abspath(lib)) if lib else json.load(open(B.ISA_OUT))).get(B.L0_KERNEL)
 
 
-def run_pass(counter, outdir):
+def run_pass(counter, outdir, groups):
     cmd = ["timeout", "-s", "KILL", "90", "rocprofv3", "--pmc", counter, "--output-format", "csv", "-d", outdir,
            "-o", "c", "--", sys.executable, os.path.join(ROOT, "tools", "kbench.py"), "--c4", "--level", "0",
-           "--mode", "level", "--from-solve", "--reps", "10", "--warm-ms", "0"]
+           "--mode", "level", "--from-solve", "--reps", "10", "--warm-ms", "0", "--groups", str(groups)]
     env = dict(os.environ, TMPDIR="/tmp")
     if env.get("DPFT_LIB"):  # a variant library (tools/build_variants.py); the profiler runs from /tmp
         env["DPFT_LIB"] = os.path.abspath(env["DPFT_LIB"])
@@ -64,11 +64,14 @@ def run_pass(counter, outdir):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--out", required=True)
+    ap.add_argument("--groups", type=int, default=4, help="8-pair batches per launch (bench.py --groups)")
     a = ap.parse_args()
     tmp = os.path.join(ROOT, "gpurun_out", "pmc_l0")
-    fetch, nf = run_pass("FETCH_SIZE", os.path.join(tmp, "fetch"))
-    write, nw = run_pass("WRITE_SIZE", os.path.join(tmp, "write"))
-    out = {"kernel": "ic_reduce_kernel<32,Cs=1,tru,U_IC,c4> level 0, B=8, 640x480 (tools/kbench.py --mode level --from-solve)",
+    fetch, nf = run_pass("FETCH_SIZE", os.path.join(tmp, "fetch"), a.groups)
+    write, nw = run_pass("WRITE_SIZE", os.path.join(tmp, "write"), a.groups)
+    out = {"kernel": f"ic_reduce_kernel<32,Cs=1,tru,U_IC,c4> level 0, {a.groups} x 8 pairs per launch, 640x480 "
+                     "(tools/kbench.py --mode level --from-solve)",
+           "pairs_per_launch": 8 * a.groups, "group": 8,
            "src_sha256": src_sha(), "isa_sha256": isa_sha(), "launches": {"fetch": nf, "write": nw},
            "FETCH_SIZE_KiB": fetch, "WRITE_SIZE_KiB": write,
            "read_bytes": 2 * 1024 * fetch, "write_bytes": 1024 * write,
