@@ -102,6 +102,13 @@ constexpr bool kMarch = DPFT_MARCH != 0;  // channel-quad reduce: row-marching w
 #define DPFT_SPLIT_MAX_PIXELS 40000
 #endif
 constexpr long kSplitMaxPixels = DPFT_SPLIT_MAX_PIXELS;  // channel-quad levels up to this size per pair: ic_split_kernel
+#ifndef DPFT_SPLIT_MAX_LAUNCH_PIXELS
+#define DPFT_SPLIT_MAX_LAUNCH_PIXELS 320000
+#endif
+// ... and up to this many pixels per launch (all pairs): a level of a grouped call
+// (DPFT_GROUP) with more fills the device as a marching launch (level 2 of 32 pairs:
+// 614 k pixels, the size of level 1 of 8 pairs, where marching is the faster schedule)
+constexpr long kSplitMaxLaunchPixels = DPFT_SPLIT_MAX_LAUNCH_PIXELS;
 #ifndef DPFT_SPLIT_SEPFIN
 #define DPFT_SPLIT_SEPFIN 1
 #endif
@@ -299,14 +306,19 @@ __device__ __forceinline__ int xcd_remap(int orig, int n) {
 // from the second, as with one pair per XCD -- the band skew assumes exactly that split.
 // Without it the second pair of an XCD ran entirely as second workgroups and finished
 // last (B = 16: 313 us per level-0 launch, 156 us per 8 pairs against 141 at B = 8).
-__device__ __forceinline__ int pair_slot_remap(int orig, int n, int nbpp) {
+// `qr`: workgroups per XCD and dispatch round (the resident grid / 8; a grid of several
+// rounds runs the pairs of round k of every XCD after those of round k - 1).
+__device__ __forceinline__ int pair_slot_remap(int orig, int n, int nbpp, int qr) {
   int kb = xcd_remap(orig, n);
   const int q = n >> 3;
-  if ((n & 7) == 0 && (nbpp & 1) == 0 && q % nbpp == 0 && q / nbpp >= 2 && (q & 1) == 0) {
-    const int xb = kb - kb % q, i = kb - xb, h = q >> 1, hp = nbpp >> 1;
-    const bool second = i >= h;
-    const int ii = second ? i - h : i, pin = ii / hp;
-    kb = xb + pin * nbpp + (ii - pin * hp) + (second ? hp : 0);
+  if ((n & 7) == 0 && qr > 0 && q % qr == 0) {
+    const int xb = kb - kb % q, i0 = kb - xb, rb = i0 - i0 % qr, i = i0 - rb;
+    if ((nbpp & 1) == 0 && qr % nbpp == 0 && qr / nbpp >= 2 && (qr & 1) == 0) {
+      const int h = qr >> 1, hp = nbpp >> 1;
+      const bool second = i >= h;
+      const int ii = second ? i - h : i, pin = ii / hp;
+      kb = xb + rb + pin * nbpp + (ii - pin * hp) + (second ? hp : 0);
+    }
   }
   return kb;
 }
@@ -449,6 +461,7 @@ struct IterParams {
   const uint32_t* ext;   // sigma0 extrema of this level (order-encoded min, max)
   float* rec;
   int nbpp, per_pair, row_groups, rps;  // reduce kernel schedule (see ic_reduce_kernel); rps = rows per step
+  int round_wg;    // reduce kernel: resident workgroups per XCD (pair_slot_remap)
   int fin_on;      // 0: records only (timing hook); 1: last workgroup finalizes
   int reverse;     // marching path: walk every band in the opposite direction (DPFT_ITER_REVERSE)
   int skew;        // marching path: band-size skew, 64ths (see ic_reduce_kernel)
@@ -1217,7 +1230,7 @@ __global__ __launch_bounds__(kThreads, DPFT_MIN_WAVES) void ic_reduce_kernel(Ite
 
   const int tid = threadIdx.x, lane = tid & 63, wave = wave_id();
   const int W = p.W, H = p.H, HW = H * W;
-  const int kb = pair_slot_remap(blockIdx.x, gridDim.x, p.nbpp);
+  const int kb = pair_slot_remap(blockIdx.x, gridDim.x, p.nbpp, p.round_wg);
   const int b = kb / p.nbpp, jb = kb - b * p.nbpp;
   const int seg_begin = b * p.per_pair + (int)(((long)p.per_pair * jb) / p.nbpp);
   const int seg_end = b * p.per_pair + (int)(((long)p.per_pair * (jb + 1)) / p.nbpp);
@@ -2961,6 +2974,7 @@ IterParams make_params(const DpftLevelDesc& d, const DpftLevelTensors& tt, const
   p.row_groups = (d.H + p.rps - 1) / p.rps;
   p.per_pair = g.tiles_x * p.row_groups;
   p.nbpp = 0;  // set at launch from the kernel's resident capacity
+  p.round_wg = 0;
   p.fin_on = 0;
   p.reverse = 0;
   p.skew = kMarchSkew;
@@ -3047,7 +3061,13 @@ int launch_reduce_k(IterParams p, hipStream_t st) {
   const void* k = reinterpret_cast<const void*>(&ic_reduce_kernel<CT, CS1, TRU, MODE, C4>);
   const int cap = resident_blocks(k);
   if (cap <= 0) return fail(DPFT_E_HIP, "occupancy query failed");
-  p.nbpp = std::max(1, std::min(cap / p.B, p.per_pair));
+  static const int rounds = [] {  // tuning only: dispatch rounds of the grid (default 1)
+    const char* e = getenv("DPFT_DEBUG_ROUNDS");
+    return e ? std::min(std::max(atoi(e), 1), 8) : 1;
+  }();
+  p.nbpp = std::max(1, std::min(cap * rounds / p.B, p.per_pair));
+  if ((long)p.B * p.nbpp > kMaxGrid) p.nbpp = std::max(1, kMaxGrid / p.B);
+  p.round_wg = cap / 8;
   p.fin.nbpp = p.nbpp;
   // finalize in-kernel (last-workgroup handshake) or as its own one-workgroup launch
   const bool sep = p.fin_on && (long)p.H * p.W <= kSepFinMaxPixels;
@@ -3097,7 +3117,8 @@ int launch_reduce_c4(const IterParams& p, hipStream_t st) {
   if constexpr (CT > 0 && CT % 16 == 0) {
     uint32_t sched = p.flags & DPFT_SCHED_MASK;
     if (sched == DPFT_SCHED_AUTO)  // coarse levels (few pixels per pair): the channel-split kernel
-      sched = ((long)p.H * p.W <= kSplitMaxPixels) ? DPFT_SCHED_SPLIT : DPFT_SCHED_MARCH;
+      sched = ((long)p.H * p.W <= kSplitMaxPixels && (long)p.B * p.H * p.W <= kSplitMaxLaunchPixels)
+                  ? DPFT_SCHED_SPLIT : DPFT_SCHED_MARCH;
     if (!(p.flags & DPFT_COMBINE_ICP) && !p.wgt) {  // combine_ICP / M-estimator weights: ic_reduce_kernel
       if (sched == DPFT_SCHED_SPLIT) {
         if (p.flags & DPFT_NO_UNCERTAINTY) return launch_split<CT, false, 2>(p, st);

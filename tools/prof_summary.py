@@ -106,7 +106,7 @@ def main():
                                                           "min_us": min(d), "max_us": max(d)}
     if one:
         t0 = one[0][0]
-        lines += ["", "## One channel-quad solve (B = 8 pairs, graph replay, nothing else in flight)\n",
+        lines += ["", "## One channel-quad solve (all pairs of one launch, graph replay, nothing else in flight)\n",
                   "| start us | duration us | level | kernel | workgroups |", "|---|---|---|---|---|"]
         for st, d, lv, name, wg in one:
             lines.append(f"| {(st - t0) / 1e3:.1f} | {d:.1f} | {lv} | {name} | {wg} |")
@@ -119,7 +119,8 @@ def main():
         out["l0_traffic"] = t
         lines += ["", "## Level-0 reduce launch: HBM traffic (separate FETCH_SIZE / WRITE_SIZE passes)\n",
                   f"read {t['read_bytes'] / 1e6:.1f} MB + write {t['write_bytes'] / 1e6:.2f} MB per launch "
-                  f"({t['correction']}); algorithmic 668.5 MB -> {t['hbm_bytes'] / 668467200:.2f}x"]
+                  f"({t['correction']}); algorithmic {668467200 * t.get('pairs_per_launch', 8) / 8 / 1e6:.1f} MB "
+                  f"({t.get('pairs_per_launch', 8)} pairs) -> {t['hbm_bytes'] / (668467200 * t.get('pairs_per_launch', 8) / 8):.2f}x"]
     open(a.out + ".md", "w").write("\n".join(lines) + "\n")
     json.dump(out, open(a.out + ".json", "w"), indent=1)
     print("\n".join(lines))
