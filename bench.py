@@ -45,10 +45,10 @@ def parse():
     p.add_argument("--setup-warm-ms", type=float, default=200.0,
                    help="setup: replay solves for this long before the --warmup steps (the GPU clock ramps over "
                         "the first tens of milliseconds of load; 5 warm-up steps are 3 ms)")
-    p.add_argument("--groups", type=int, default=4,
+    p.add_argument("--groups", type=int, default=16,
                    help="independent B-pair batches per launch (DPFT_GROUP): each solved as its own call -- its "
                         "own batch-global truncated-sigma extrema -- in launches covering all of them")
-    p.add_argument("--inflight", type=int, default=4,
+    p.add_argument("--inflight", type=int, default=1,
                    help="grouped solves in flight per GPU (one stream, graph, workspace and input set each)")
     p.add_argument("--kernel-reps", type=int, default=50)
     p.add_argument("--no-cpu-baseline", action="store_true")

@@ -465,6 +465,7 @@ struct IterParams {
   int fin_on;      // 0: records only (timing hook); 1: last workgroup finalizes
   int reverse;     // marching path: walk every band in the opposite direction (DPFT_ITER_REVERSE)
   int skew;        // marching path: band-size skew, 64ths (see ic_reduce_kernel)
+  int grid_waste;  // marching path: idle waves (64ths of a pair's) the band grid may leave
   FinParams fin;
 };
 
@@ -1492,7 +1493,7 @@ __global__ __launch_bounds__(kThreads, DPFT_MIN_WAVES) void ic_reduce_kernel(Ite
     // L2 hit for the second) instead of tens of microseconds apart.  Up to nw / 16 waves
     // may be left without a band (nw - K S); otherwise the strip-major split below.
     const int S_ = p.tiles_x, K_ = nw / S_;
-    const bool grid = kMarchGrid && K_ >= 2 && (nw - K_ * S_) * 16 <= nw;
+    const bool grid = kMarchGrid && K_ >= 2 && (nw - K_ * S_) * 64 <= nw * p.grid_waste;
     int ubeg, uend, vband;
     if (grid) {
       const int k = band / S_, s = band - k * S_;
@@ -2983,6 +2984,11 @@ IterParams make_params(const DpftLevelDesc& d, const DpftLevelTensors& tt, const
     return e ? std::min(std::max(atoi(e), 0), 63) : -1;
   }();
   if (skew_env >= 0) p.skew = skew_env;
+  static const int waste_env = [] {  // tuning only
+    const char* e = getenv("DPFT_DEBUG_GRID_WASTE");
+    return e ? std::min(std::max(atoi(e), 0), 63) : 4;
+  }();
+  p.grid_waste = waste_env;
   memset(&p.fin, 0, sizeof(p.fin));
   p.fin.rec = p.rec;
   p.fin.prec = reinterpret_cast<double*>(static_cast<char*>(ws) + kCtrlBytes);

@@ -25,7 +25,7 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 SRC = os.path.join(ROOT, "deep_prob_feature_track_amd", "csrc", "dpft_ic.hip")
 
 
-SOLVE_LAUNCHES = 6
+LEVEL0_LAUNCHES = 1 + 3 * 10  # kbench --mode level --reps 10
 
 
 def src_sha():
@@ -48,14 +48,19 @@ def run_pass(counter, outdir, groups):
     if env.get("DPFT_LIB"):  # a variant library (tools/build_variants.py); the profiler runs from /tmp
         env["DPFT_LIB"] = os.path.abspath(env["DPFT_LIB"])
     subprocess.run(cmd, check=True, cwd="/tmp", env=env)
+    return parse(counter, outdir)
+
+
+def parse(counter, outdir):
     rows = []
     for f in glob.glob(os.path.join(outdir, "**", "*counter_collection.csv"), recursive=True):
         for r in csv.DictReader(open(f)):
             if "ic_reduce_kernel" in r["Kernel_Name"] and r["Counter_Name"] == counter:
                 rows.append((int(r["Dispatch_Id"]), float(r["Counter_Value"])))
-    # the first SOLVE_LAUNCHES marching launches belong to kbench's --from-solve pyramid
-    # solve (levels 1 and 0, three each): not the timed level-0 group
-    vals = [v for _, v in sorted(rows)[SOLVE_LAUNCHES:]]
+    # the last LEVEL0_LAUNCHES are kbench's level-0 launches (its first iteration + reps x 3);
+    # before them, its --from-solve pyramid solve (marching launches per level depend on
+    # the batch size: levels 1 and 0 at 8 pairs, every level at 128)
+    vals = [v for _, v in sorted(rows)[-LEVEL0_LAUNCHES:]]
     if not vals:
         raise SystemExit(f"no ic_reduce_kernel rows for {counter}")
     return sum(vals) / len(vals), len(vals)
@@ -64,11 +69,16 @@ def run_pass(counter, outdir, groups):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--out", required=True)
-    ap.add_argument("--groups", type=int, default=4, help="8-pair batches per launch (bench.py --groups)")
+    ap.add_argument("--groups", type=int, default=16, help="8-pair batches per launch (bench.py --groups)")
+    ap.add_argument("--from-dir", help="parse the fetch/ and write/ CSVs under this directory instead of running")
     a = ap.parse_args()
     tmp = os.path.join(ROOT, "gpurun_out", "pmc_l0")
-    fetch, nf = run_pass("FETCH_SIZE", os.path.join(tmp, "fetch"), a.groups)
-    write, nw = run_pass("WRITE_SIZE", os.path.join(tmp, "write"), a.groups)
+    if a.from_dir:  # re-read the CSVs of an earlier run (same launch shape)
+        fetch, nf = parse("FETCH_SIZE", os.path.join(a.from_dir, "fetch"))
+        write, nw = parse("WRITE_SIZE", os.path.join(a.from_dir, "write"))
+    else:
+        fetch, nf = run_pass("FETCH_SIZE", os.path.join(tmp, "fetch"), a.groups)
+        write, nw = run_pass("WRITE_SIZE", os.path.join(tmp, "write"), a.groups)
     out = {"kernel": f"ic_reduce_kernel<32,Cs=1,tru,U_IC,c4> level 0, {a.groups} x 8 pairs per launch, 640x480 "
                      "(tools/kbench.py --mode level --from-solve)",
            "pairs_per_launch": 8 * a.groups, "group": 8,
