@@ -473,8 +473,11 @@ def _invalid_counts(solver, level, R, t):
 
 
 @pytest.mark.gpu
-def test_grouped_batches_solve_as_separate_calls():
-    """DPFT_GROUP (bench.py --groups): 4 independent 8-pair batches in every launch.  Each
+@pytest.mark.parametrize("G", [4, 16])
+def test_grouped_batches_solve_as_separate_calls(G):
+    """DPFT_GROUP (bench.py --groups): G independent 8-pair batches in every launch (16 is
+    the bench's operating point: 4 workgroups = 16 waves per pair, fewer than two per
+    level-0 strip, so the marching bands are not a (row band x strip) grid).  Each
     batch is solved as a call of its own -- its own truncated-sigma extrema: the invalid
     pixel counts equal those of separate 8-pair calls exactly (and differ from one
     32-pair batch, whose extrema span all four), the poses within the fp32 summation
@@ -482,7 +485,7 @@ def test_grouped_batches_solve_as_separate_calls():
     golden pair, unscaled) lands on the reference's poses."""
     from deep_prob_feature_track_amd import ic
     dev = _dev()
-    G, B = 4, 8
+    B = 8
     z, levels, K, R0, t0 = _grouped_case(dev, G, B)
     grouped = ic.PyramidSolver(levels, K, iters=3, remove_tru_sigma=True, group=B)
     assert grouped.group == B
