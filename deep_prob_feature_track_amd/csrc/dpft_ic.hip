@@ -138,6 +138,13 @@ constexpr int kMarchSkew = DPFT_MARCH_SKEW;  // band-size skew of the marching s
 // marching bands on a (row band x strip) grid: every strip cut at the same rows, so the
 // waves of horizontally adjacent strips read their shared columns at the same time
 constexpr bool kMarchGrid = DPFT_MARCH_GRID != 0;
+#ifndef DPFT_MARCH_HYBRID
+#define DPFT_MARCH_HYBRID 1
+#endif
+// S < waves < 2 S per pair (level 0 of a 128-pair launch: 16 waves over 11 strips): wave
+// s < S marches the top rows of strip s (common row cuts per weight class), the other
+// waves split the strips' bottom rows strip-major
+constexpr bool kMarchHybrid = DPFT_MARCH_HYBRID != 0;
 constexpr int kMarchRows = DPFT_MARCH_ROWS;  // rows per marching step (1, or 2: -10 % f1 traffic, +11 % VALU, 4 % slower)
 constexpr int kRingM = DPFT_RING_M;       // quads in flight on the marching path (kRingM - 1 ahead)
 #ifndef DPFT_UNROLL_Q
@@ -1495,7 +1502,32 @@ __global__ __launch_bounds__(kThreads, DPFT_MIN_WAVES) void ic_reduce_kernel(Ite
     const int S_ = p.tiles_x, K_ = nw / S_;
     const bool grid = kMarchGrid && K_ >= 2 && (nw - K_ * S_) * 64 <= nw * p.grid_waste;
     int ubeg, uend, vband;
-    if (grid) {
+    // hybrid split: wave s < S owns rows [0, T_s) of strip s, T_s its weighted share of
+    // the pair's units (Tf for the first half of the waves, Tu for the second); the
+    // nw - S pool waves split the bottom rows [T_s, H) of all strips, strip-major
+    const bool hyb = kMarchHybrid && !grid && nw > S_ && nw < 2 * S_;
+    const int hh = nw >> 1, hsk = nw >= 2 ? p.skew : 0;
+    const int hwt = (64 + hsk) * hh + (64 - hsk) * (nw - hh);
+    const int hTf = min(H, (U * (64 + hsk)) / hwt), hTu = min(H, (U * (64 - hsk)) / hwt);
+    const int hnf = min(hh, S_), hLf = H - hTf, hLu = H - hTu;
+    const bool hpool = hyb && band >= S_;
+    if (hyb && !hpool) {
+      ubeg = band * H;
+      uend = band * H + (band < hh ? hTf : hTu);
+      vband = 0;
+    } else if (hpool) {
+      const int PU = hnf * hLf + (S_ - hnf) * hLu, np = nw - S_, j = band - S_;
+      int wt = 0, ws0 = 0, ws1 = 0;  // weighted split over the pool waves S .. nw - 1
+      for (int i = 0; i < np; ++i) {
+        const int wi = (S_ + i) < hh ? 64 + hsk : 64 - hsk;
+        wt += wi;
+        ws0 += i < j ? wi : 0;
+        ws1 += i <= j ? wi : 0;
+      }
+      ubeg = (PU * ws0) / wt;
+      uend = (PU * ws1) / wt;
+      vband = 1;
+    } else if (grid) {
       const int k = band / S_, s = band - k * S_;
       ubeg = k < K_ ? s * H + split_start(k, K_, H) : 0;
       uend = k < K_ ? s * H + split_start(k + 1, K_, H) : 0;
@@ -1511,12 +1543,33 @@ __global__ __launch_bounds__(kThreads, DPFT_MIN_WAVES) void ic_reduce_kernel(Ite
     const bool up = ((vband & 1) != 0) != (kMarchReverse && p.reverse != 0);
     const int dir = up ? -1 : 1;
     const float dirf = up ? -1.0f : 1.0f;
-    const int row_restart = up ? H - 1 : 0;  // a strip begins here in marching order
-    auto unit_pos = [&](int k, int& xs, int& y) {
+    // unit k of the wave's run -> (lane column xs, row y); strt: a strip begins at this
+    // row in marching order (row H - 1 marching up, the strip's first row marching down)
+    auto unit_pos_st = [&](int k, int& xs, int& y, bool& strt) {
       const int u = up ? uend - 1 - k : ubeg + k;
-      const int strip = u / H;
-      y = u - strip * H;
+      int strip, ytop = 0;
+      if (hpool) {
+        const int uf = hnf * hLf;
+        if (u < uf) {
+          strip = u / max(hLf, 1);
+          y = hTf + (u - strip * hLf);
+          ytop = hTf;
+        } else {
+          const int s2 = (u - uf) / max(hLu, 1);
+          y = hTu + (u - uf - s2 * hLu);
+          strip = hnf + s2;
+          ytop = hTu;
+        }
+      } else {
+        strip = u / H;
+        y = u - strip * H;
+      }
+      strt = y == (up ? H - 1 : ytop);
       xs = strip * kTileOut - 1 + lane;
+    };
+    auto unit_pos = [&](int k, int& xs, int& y) {
+      bool strt;
+      unit_pos_st(k, xs, y, strt);
     };
     // window in LDS, per wave [2 slots][NQ quads][64 lanes] (each lane only ever touches
     // its own column and a wave's LDS accesses complete in order: no barrier)
@@ -1558,7 +1611,8 @@ __global__ __launch_bounds__(kThreads, DPFT_MIN_WAVES) void ic_reduce_kernel(Ite
       constexpr int NS = decltype(NSC)::value;
       constexpr int NU = NQW * NS;
       int xs, yr[NS];
-      unit_pos(k, xs, yr[0]);
+      bool strt0;
+      unit_pos_st(k, xs, yr[0], strt0);
       if constexpr (NS == 2) {
         int xs1;
         unit_pos(k + 1, xs1, yr[1]);
@@ -1566,7 +1620,7 @@ __global__ __launch_bounds__(kThreads, DPFT_MIN_WAVES) void ic_reduce_kernel(Ite
       const float dcur[2] = {dnx[0], dnx[1]};
       if (k + NS < nrows) load_d2(k + NS, dnx);
       const int colq = min(max(xs, 0), W - 1) * 16;
-      if (k == 0 || yr[0] == row_restart) {  // prime the window: rows y - dir (replicate-clamped) and y
+      if (k == 0 || strt0) {  // prime the window: rows y - dir (replicate-clamped) and y
         const int yp = min(max(yr[0] - dir, 0), H - 1);
 #pragma unroll
         for (int q = 0; q < NQW; ++q) {
@@ -1801,8 +1855,9 @@ __global__ __launch_bounds__(kThreads, DPFT_MIN_WAVES) void ic_reduce_kernel(Ite
       bool two = kMarchRows == 2 && k + 1 < nrows;
       if (two) {
         int xs1, y1;
-        unit_pos(k + 1, xs1, y1);
-        two = y1 != row_restart;
+        bool strt1;
+        unit_pos_st(k + 1, xs1, y1, strt1);
+        two = !strt1;
       }
       if (two) {
         stepn(WaveIdx<2>{}, k);
