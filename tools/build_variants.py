@@ -1,5 +1,6 @@
 """Build compile-time variants of libdpft_ic.so under tools/libs/ for A/B runs on the GPU box
-(select one with DPFT_LIB=tools/libs/libdpft_<name>.so; tools/kbench.py honours it).
+(select one with DPFT_LIB=tools/libs/libdpft_<name>.so; tools/kbench.py, bench.py and
+tools/variant_pytest.py honour it).
 
 python tools/build_variants.py name=-DFLAG=V[,-DFLAG2=V] ...
 """
