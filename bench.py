@@ -1,25 +1,26 @@
 #!/usr/bin/env python
 """Benchmark: IC solver iterations/s, 640x480, C=32, 4-level pyramid (BASELINE.json).
 
-One *step* = one full coarse-to-fine solve (levels 3..0, 3 Gauss-Newton
-iterations each = 12 IC iterations per pair) of G independent batches of B frame
-pairs per GPU (--groups G, --batch-per-gpu B), replayed from one HIP graph, followed
-(N > 1) by the RCCL all-gather of the per-pair poses.  The G batches share every
-launch (DPFT_GROUP: each batch keeps its own batch-global truncated-sigma extrema and
-is solved exactly as a call of its own), so the per-launch ramp, finish spread and
-finalize are paid once per G batches.  An eval stream keeps --inflight such grouped
-solves in flight per GPU (distinct pairs each): step k replays slot k % inflight's
-graph on that slot's stream, so one solve's latency-bound coarse levels overlap
-another's bandwidth-bound level 0.  `latency_ms_per_solve` is one grouped solve with
-nothing else in flight.  Workload: cfg3's shard -- B = 8 pairs per GPU per batch,
-cycled from the ordered pairs of the five TUM fr1/desk frames, deterministic features
-(tests/golden/recipe.py), inputs resident in HBM before the timed region.
+Workload (default, cfg3): an eval stream of global batches of 64 frame pairs; one *step* =
+one global batch, sharded contiguously over the N ranks (64 / N pairs each, strong
+scaling), each rank solving its shard as independent batches of B = 8 pairs (one
+reference call each: its own batch-global truncated-sigma extrema) in ONE grouped call
+(DPFT_GROUP): levels 3..0, 3 Gauss-Newton iterations each = 12 IC iterations per pair,
+replayed from one HIP graph, then (N > 1) the RCCL all-gather of the per-pair poses.
+`--inflight S` keeps S consecutive global batches of the stream in flight per GPU (one
+stream, graph and input set each), so one batch's latency-bound coarse levels overlap the
+next one's bandwidth-bound level 0.  `--pairs-per-gpu P` switches to weak scaling (P
+pairs per GPU per step).  `--icp`: cfg5, the same with the combine_ICP term.
 
-`value` = all-level IC iterations/s over the whole job = N * G * B * 12 / step time.
-Launch: python bench.py [--gpus N --steps K --warmup W]; for N > 1 under
+Pairs are cycled from the 20 ordered pairs of the five TUM fr1/desk frames, features are
+the deterministic recipe of tests/golden/recipe.py (the checkpoints are absent), inputs
+are resident in HBM (channel-quad layout) before the timed region.
+`value` = all-level IC iterations/s of the whole job = pairs per step * 12 / step time.
+Launch: python bench.py [--gpus N --steps K --warmup W]; N > 1 under
 torch.distributed.run (one rank per GPU, RCCL).
 """
 import argparse
+import ctypes
 import json
 import os
 import sys
@@ -41,106 +42,108 @@ def parse():
     p.add_argument("--gpus", type=int, default=1)
     p.add_argument("--steps", type=int, default=100)
     p.add_argument("--warmup", type=int, default=10)
-    p.add_argument("--batch-per-gpu", type=int, default=8)
+    p.add_argument("--global-batch", type=int, default=64,
+                   help="pairs per step over all ranks (cfg3: 64), sharded contiguously -- strong scaling")
+    p.add_argument("--pairs-per-gpu", type=int, default=0,
+                   help="> 0: weak scaling instead, this many pairs per GPU per step")
+    p.add_argument("--batch", type=int, default=8,
+                   help="pairs per independent batch (one reference call: its own batch-global extrema)")
+    p.add_argument("--inflight", type=int, default=2,
+                   help="consecutive steps of the stream in flight per GPU (one stream, graph, workspace each)")
+    p.add_argument("--icp", action="store_true", help="cfg5: with the combine_ICP term (weight 0.01)")
     p.add_argument("--setup-warm-ms", type=float, default=200.0,
                    help="setup: replay solves for this long before the --warmup steps (the GPU clock ramps over "
-                        "the first tens of milliseconds of load; 5 warm-up steps are 3 ms)")
-    p.add_argument("--groups", type=int, default=16,
-                   help="independent B-pair batches per launch (DPFT_GROUP): each solved as its own call -- its "
-                        "own batch-global truncated-sigma extrema -- in launches covering all of them")
-    p.add_argument("--inflight", type=int, default=1,
-                   help="grouped solves in flight per GPU (one stream, graph, workspace and input set each)")
-    p.add_argument("--kernel-reps", type=int, default=50)
+                        "the first tens of milliseconds of load)")
+    p.add_argument("--kernel-reps", type=int, default=30)
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--no-graph", action="store_true")
     p.add_argument("--layout", choices=["c4", "nchw"], default="c4",
                    help="resident feature layout the timed solve reads (c4: channel-quad, the solver's native one)")
-    p.add_argument("--no-compare", action="store_true", help="skip the secondary timing of the other layout")
+    p.add_argument("--no-compare", action="store_true", help="skip the secondary timings (other layout, end-to-end)")
     return p.parse_args()
 
 
-def make_group_inputs(B, G, first, device):
-    """G independent B-pair batches (make_inputs `first` .. `first` + G - 1) stacked along
-    the pair axis: batch g is pairs [g B, (g + 1) B) of one DPFT_GROUP(B) call."""
-    parts = [make_inputs(B, first + g, device) for g in range(G)]
-    if G == 1:
-        return parts[0]
-    sel = [p for part in parts for p in part[0]]
-    levels = [{k: torch.cat([part[1][l][k] for part in parts]) for k in parts[0][1][l]} for l in range(LEVELS)]
-    return sel, levels, torch.cat([part[2] for part in parts])
-
-
-def make_inputs(B, rank, device):
+# ---------------------------------------------------------------------------- inputs
+def make_batches(B, first, count, device, icp=False):
+    """`count` consecutive independent batches of B pairs, batch q (q = first .. first +
+    count - 1) holding ordered pairs q B .. q B + B - 1 (cycled through the 20 of the five
+    frames), stacked along the pair axis: (pairs, per-level NCHW dicts, K [count B, 4])."""
     import recipe
-    pairs = [(i, j) for i in range(5) for j in range(5) if i != j]
-    sel = [pairs[(rank * B + k) % len(pairs)] for k in range(B)]
-    feat = {}
-
-    def fs(idx, l):
-        if (idx, l) not in feat:
-            feat[(idx, l)] = recipe.features(idx, C, l)
-        return feat[(idx, l)]
-
-    inv0 = recipe.inv_depth_batch([recipe.depth_m(i) for i, _ in sel])
-    inv1 = recipe.inv_depth_batch([recipe.depth_m(j) for _, j in sel])
-    levels = []
-    for l in range(LEVELS):
-        k = 1 << l
-        dev = lambda a: torch.from_numpy(np.ascontiguousarray(a)).to(device)
-        levels.append(dict(
-            x0=dev(np.stack([fs(i, l)[0] for i, _ in sel])), x1=dev(np.stack([fs(j, l)[0] for _, j in sel])),
-            sigma0=dev(np.stack([fs(i, l)[1] for i, _ in sel])), sigma1=dev(np.stack([fs(j, l)[1] for _, j in sel])),
-            invD0=dev(recipe.max_pool(inv0, k)), invD1=dev(recipe.max_pool(inv1, k))))
-    K = torch.from_numpy(np.tile(recipe.K_FULL[None], (B, 1))).to(device)
+    sel, levels = [], [dict() for _ in range(LEVELS)]
+    for q in range(first, first + count):
+        bsel = [recipe.ORDERED_PAIRS[(q * B + k) % len(recipe.ORDERED_PAIRS)] for k in range(B)]
+        sel += bsel
+        d0 = [recipe.depth_m(i) for i, _ in bsel]
+        d1 = [recipe.depth_m(j) for _, j in bsel]
+        inv0, inv1 = recipe.inv_depth_batch(d0), recipe.inv_depth_batch(d1)  # per reference call
+        for l in range(LEVELS):
+            k = 1 << l
+            part = dict(x0=np.stack([recipe.features(i, C, l)[0] for i, _ in bsel]),
+                        x1=np.stack([recipe.features(j, C, l)[0] for _, j in bsel]),
+                        sigma0=np.stack([recipe.features(i, C, l)[1] for i, _ in bsel]),
+                        sigma1=np.stack([recipe.features(j, C, l)[1] for _, j in bsel]),
+                        invD0=recipe.max_pool(inv0, k), invD1=recipe.max_pool(inv1, k))
+            if icp:
+                part["depth0"] = recipe.max_pool(np.stack(d0)[:, None], k)
+                part["depth1"] = recipe.max_pool(np.stack(d1)[:, None], k)
+            for key, v in part.items():
+                levels[l].setdefault(key, []).append(v)
+    dev = lambda a: torch.from_numpy(np.ascontiguousarray(np.concatenate(a))).to(device)
+    levels = [{k: dev(v) for k, v in d.items()} for d in levels]
+    K = torch.from_numpy(np.tile(recipe.K_FULL[None], (B * count, 1))).to(device)
     return sel, levels, K
 
 
-def l0_traffic(pairs, group):
-    """Per-launch HBM bytes of the level-0 reduce launch from the committed PMC
-    measurement (tools/pmc_l0.py: separate FETCH_SIZE / WRITE_SIZE rocprofv3 passes,
-    gfx950-corrected), used only if it was measured on the machine code of the kernel
-    built here (the ISA hash build.py records beside the library; the source file's hash
-    for measurements that predate it)."""
+def l0_traffic(pairs, group, kernel):
+    """Per-launch HBM bytes of the level-0 reduce launch from the committed PMC measurement
+    (tools/pmc_l0.py: separate FETCH_SIZE / WRITE_SIZE rocprofv3 passes, gfx950-corrected),
+    used only if it was measured on the machine code of the kernel built here (the ISA hash
+    build.py records beside the library) and on the same launch shape."""
     import glob
-    import hashlib
-    from deep_prob_feature_track_amd import build as B
-    src = os.path.join(ROOT, "deep_prob_feature_track_amd", "csrc", "dpft_ic.hip")
-    sha = hashlib.sha256(open(src, "rb").read()).hexdigest()
-    isa = json.load(open(B.ISA_OUT)).get(B.L0_KERNEL) if os.path.exists(B.ISA_OUT) else None
+    from deep_prob_feature_track_amd import build as Bd
+    isa = json.load(open(Bd.ISA_OUT)).get(kernel) if os.path.exists(Bd.ISA_OUT) else None
+    if isa is None:
+        return None
     for f in sorted(glob.glob(os.path.join(ROOT, "profiles", "*_l0_traffic.json")), reverse=True):
         d = json.load(open(f))
-        if d.get("pairs_per_launch", 8) != pairs or d.get("group", pairs) != group:
-            continue  # measured on another launch shape
-        if (isa is not None and d.get("isa_sha256") == isa) or d.get("src_sha256") == sha:
+        if d.get("pairs_per_launch", 8) == pairs and d.get("group", pairs) == group and d.get("isa_sha256") == isa:
             return {"hbm_bytes": d["hbm_bytes"], "source": os.path.relpath(f, ROOT)}
     return None
 
 
-def copy_peak_gbs(device, nbytes=1 << 30, reps=5):
-    """Measured HBM copy rate (torch's copy kernel, read + write bytes / time): the
-    practical ceiling SURVEY.md 8(d) asks the roofline to be reported against too."""
-    x = torch.empty(nbytes // 4, dtype=torch.float32, device=device)
-    y = torch.empty_like(x)
-    x.fill_(1.0)
-    for _ in range(2):
-        y.copy_(x)
+def _timed(fn, reps, device):
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     e0.record()
     for _ in range(reps):
-        y.copy_(x)
+        fn()
     e1.record()
-    torch.cuda.synchronize()
-    gbs = 2 * nbytes * reps / (e0.elapsed_time(e1) * 1e-3) / 1e9
+    torch.cuda.synchronize(device)
+    return e0.elapsed_time(e1) * 1e-3 / reps
+
+
+def copy_peak_gbs(device, nbytes=1 << 30, reps=10):
+    """Measured HBM copy ceiling: the library's float4 copies (dpft_copy_probe: one 16-byte
+    element per thread, and a grid-stride non-temporal variant), read + write bytes / time of
+    the faster."""
+    from deep_prob_feature_track_amd import _native as N, ic
+    L = N.lib()
+    x = torch.ones(nbytes // 4, dtype=torch.float32, device=device)
+    y = torch.empty_like(x)
+    st = ctypes.c_void_p(torch.cuda.current_stream(device).cuda_stream)
+    best = 0.0
+    for mode in (0, 1):
+        run = lambda: N.check(L.dpft_copy_probe(ic._ptr(x), ic._ptr(y), nbytes, mode, st), "copy probe")
+        for _ in range(3):
+            run()
+        best = max(best, 2 * nbytes / _timed(run, reps, device) / 1e9)
     del x, y
-    return gbs
+    return best
 
 
 def read_peak_gbs(device, nbytes, reps=10):
-    """Measured HBM read ceiling: the library's diagnostic streaming read
-    (dpft_read_probe: 16-byte loads, four in flight per lane, 4096 workgroups) over a
-    buffer of the level-0 launch's algorithmic size, plain and non-temporal loads;
-    returns the faster, in GB/s."""
-    import ctypes
+    """Measured HBM read ceiling: dpft_read_probe (16-byte loads, four in flight per lane)
+    over a buffer of the level-0 launch's algorithmic size, plain and non-temporal loads;
+    the faster, in GB/s."""
     from deep_prob_feature_track_amd import _native as N, ic
     L = N.lib()
     buf = torch.ones(nbytes // 4, dtype=torch.float32, device=device)
@@ -148,15 +151,10 @@ def read_peak_gbs(device, nbytes, reps=10):
     st = ctypes.c_void_p(torch.cuda.current_stream(device).cuda_stream)
     best = 0.0
     for nt in (0, 1):
+        run = lambda: N.check(L.dpft_read_probe(ic._ptr(buf), buf.numel() * 4, nt, ic._ptr(out), st), "read probe")
         for _ in range(3):
-            N.check(L.dpft_read_probe(ic._ptr(buf), buf.numel() * 4, nt, ic._ptr(out), st), "read probe")
-        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-        e0.record()
-        for _ in range(reps):
-            N.check(L.dpft_read_probe(ic._ptr(buf), buf.numel() * 4, nt, ic._ptr(out), st), "read probe")
-        e1.record()
-        torch.cuda.synchronize()
-        best = max(best, buf.numel() * 4 * reps / (e0.elapsed_time(e1) * 1e-3) / 1e9)
+            run()
+        best = max(best, buf.numel() * 4 / _timed(run, reps, device) / 1e9)
     del buf, out
     return best
 
@@ -171,53 +169,90 @@ def cpu_model():
     return "unknown"
 
 
-def cpu_solve_seconds(lv, Kc, threads):
-    """One oracle solve of one pair on `threads` host threads (no warm-up)."""
+def host_cpus():
+    """CPUs this process may use: its affinity set, capped by the cgroup CPU quota (a GPU box
+    grants a share of the host; os.cpu_count() is the whole machine, and that many threads on
+    a 16-CPU quota spin far slower than 16)."""
+    try:
+        n = len(os.sched_getaffinity(0))
+    except (AttributeError, OSError):
+        n = os.cpu_count() or 1
+    try:
+        quota, period = open("/sys/fs/cgroup/cpu.max").read().split()[:2]
+        if quota != "max":
+            n = min(n, max(1, int(int(quota) / int(period))))
+    except (OSError, ValueError):
+        pass
+    return n
+
+
+def log(msg):
+    print(f"[bench] {msg}", file=sys.stderr, flush=True)
+
+
+# ---------------------------------------------------------------------------- parity + CPU baseline
+def oracle_solve(lv_cpu, Kc, threads, icp):
+    """One oracle solve (PyramidSolver's schedule) of the given batch on `threads` host
+    threads; (R, t, seconds)."""
     from oracle import ic_oracle as O
     old = torch.get_num_threads()
     torch.set_num_threads(threads)
     try:
+        B = Kc.shape[0]
         with torch.no_grad():
             t_start = time.perf_counter()
-            O.solve_pyramid(torch.eye(3)[None], torch.zeros(1, 3, 1), lv, Kc, iters=ITERS, remove_tru_sigma=True)
-            return time.perf_counter() - t_start
+            R, t = O.solve_pyramid(torch.eye(3).repeat(B, 1, 1), torch.zeros(B, 3, 1), lv_cpu, Kc, iters=ITERS,
+                                   remove_tru_sigma=True, combine_icp=icp)
+            return R, t.view(B, 3), time.perf_counter() - t_start
     finally:
         torch.set_num_threads(old)
 
 
-def cpu_baseline(levels_gpu, K, R_gpu, t_gpu):
-    """Oracle (PyTorch-CPU restatement of the reference solver) on pair 0: 1 warm-up, best of 2."""
-    from oracle import ic_oracle as O
-    lv = [{k: v[:1].cpu() for k, v in d.items()} for d in levels_gpu]
-    lv = [dict(f0=d["x0"], f1=d["x1"], s0=d["sigma0"], s1=d["sigma1"], invD0=d["invD0"], invD1=d["invD1"]) for d in lv]
-    Kc = K[:1].cpu()
-    R0 = torch.eye(3)[None]
-    t0 = torch.zeros(1, 3, 1)
-    best = float("inf")
-    out = None
-    with torch.no_grad():
-        for rep in range(3):
-            t_start = time.perf_counter()
-            out = O.solve_pyramid(R0, t0, lv, Kc, iters=ITERS, remove_tru_sigma=True)
-            el = time.perf_counter() - t_start
-            if rep > 0:
-                best = min(best, el)
-    one_thread = cpu_solve_seconds(lv, Kc, 1)
-    Ro, to = out
-    dR = (R_gpu[:1].cpu() - Ro).abs().max().item()
-    dt = (t_gpu[:1].cpu().view(1, 3) - to.view(1, 3)).abs().max().item()
-    # 3D end-point error between the two poses over frame-0 points (criterions.py:101-136)
+def cpu_baseline(levels_gpu, K, R_gpu, t_gpu, B, icp):
+    """The oracle (PyTorch-CPU restatement of algorithms.py:611-723) on batch 0 of slot 0 --
+    the same B pairs, one reference call, so the batch-global extrema match the GPU's batch
+    -- at every available host CPU (one run: the sample), and one pair on one thread.
+    Parity over all B pairs: max |dR|, |dt|, 3D EPE and translational RPE between the GPU
+    and the oracle poses; and the GPU poses against the reference's own run of this batch
+    (tests/golden/cfg3_b8_640x480_c32.npz) when the batch is that fixture's."""
     from deep_prob_feature_track_amd.metrics import epe3d_between, rpe
+    cpu = lambda d: {k: v[:B].cpu() for k, v in d.items()}
+    lv = [dict(f0=d["x0"], f1=d["x1"], s0=d["sigma0"], s1=d["sigma1"], invD0=d["invD0"], invD1=d["invD1"],
+               **({"depth0": d["depth0"], "depth1": d["depth1"]} if icp else {})) for d in map(cpu, levels_gpu)]
+    Kc = K[:B].cpu()
+    threads = host_cpus()
+    Ro, to, sec = oracle_solve(lv, Kc, threads, icp)
+    lv1 = [{k: v[:1] for k, v in d.items()} for d in lv]  # timing sample only
+    _, _, sec1 = oracle_solve(lv1, Kc[:1], 1, icp)
+    Rg, tg = R_gpu[:B].cpu(), t_gpu[:B].cpu().view(B, 3)
     d0 = 1.0 / lv[0]["invD0"].clamp(min=1e-6)
-    epe = epe3d_between(R_gpu[:1].cpu(), t_gpu[:1].cpu().view(1, 3), Ro, to.view(1, 3), d0,
-                        Kc, invalid=(lv[0]["invD0"] <= 0)).item()
-    # translational relative pose error between the two estimates (criterions.py
-    # compute_RPE_loss; its angle term is floored at acos(1 - 1e-7) = 4.5e-4 rad by the
-    # reference's clamp, so the rotation is reported as max |dR| above)
-    _, trs = rpe(R_gpu[:1].cpu(), t_gpu[:1].cpu().view(1, 3), Ro, to.view(1, 3))
-    return best, dR, dt, epe, one_thread, trs.item()
+    epe = epe3d_between(Rg, tg, Ro, to, d0, Kc, invalid=(lv[0]["invD0"] <= 0))
+    _, trs = rpe(Rg, tg, Ro, to)
+    out = {"value": B * LEVELS * ITERS / sec, "unit": "IC iterations/s", "cores": threads, "kind": "port",
+           "cpu_model": cpu_model(), "os_cpu_count": os.cpu_count(),
+           "sample": f"one oracle solve of the {B}-pair batch 0 (640x480 C=32, 4 levels x 3 iters, "
+                     f"{'combine_ICP, ' if icp else ''}oracle/ic_oracle.py), {threads} threads",
+           "seconds_per_batch": sec, "value_1_thread": LEVELS * ITERS / sec1,
+           "sample_1_thread": "one pair, one thread", "seconds_per_pair_1_thread": sec1,
+           "parity_pairs": B,
+           "gpu_vs_oracle_max_abs_dR": (Rg - Ro).abs().max().item(),
+           "gpu_vs_oracle_max_abs_dt": (tg - to).abs().max().item(),
+           "gpu_vs_oracle_3dpe_m_max": epe.max().item(), "gpu_vs_oracle_3dpe_m_mean": epe.mean().item(),
+           "gpu_vs_oracle_rpe_trans_m_max": trs.max().item()}
+    golden = os.path.join(ROOT, "tests", "golden", "cfg3_b8_640x480_c32.npz")
+    if not icp and B == 8 and os.path.exists(golden):
+        import recipe
+        z = np.load(golden, allow_pickle=False)
+        if [tuple(p) for p in recipe.CASES["cfg3_b8_640x480_c32"]["pairs"]] == \
+                [recipe.ORDERED_PAIRS[k] for k in range(8)]:
+            for prec in ("f32", "f64"):
+                out[f"gpu_vs_reference_{prec}_max_abs_dR"] = float(np.abs(Rg.numpy() - z[f"{prec}_R"][-1]).max())
+                out[f"gpu_vs_reference_{prec}_max_abs_dt"] = float(np.abs(tg.numpy() - z[f"{prec}_t"][-1]).max())
+            out["reference_fixture"] = "tests/golden/cfg3_b8_640x480_c32.npz (the reference's own run of batch 0)"
+    return out
 
 
+# ---------------------------------------------------------------------------- main
 def main():
     a = parse()
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -236,233 +271,235 @@ def main():
     if os.environ.get("DPFT_LIB"):  # A/B runs of compile-time variants (tools/build_variants.py)
         from deep_prob_feature_track_amd import _native
         _native.LIB_PATH = os.path.abspath(os.environ["DPFT_LIB"])
-    from deep_prob_feature_track_amd import ic, shard
+    from deep_prob_feature_track_amd import build as Bd, ic, shard
 
-    B = a.batch_per_gpu
-    G = max(1, a.groups)
     S = max(1, a.inflight)
-    BG = B * G  # pairs per launch
-    # batch g of slot j of this rank: the pairs of make_inputs "rank" (rank * S + j) * G + g
-    # (distinct pairs per batch, slot and rank, cycled through the 20 ordered pairs of the 5 frames)
-    slot_inputs = [make_group_inputs(B, G, (rank * S + j) * G, device) for j in range(S)]
+    weak = a.pairs_per_gpu > 0
+    if weak:
+        n_r = a.pairs_per_gpu
+        per_step = world * n_r
+        first = lambda j: (rank * S + j) * max(1, n_r // a.batch)
+    else:
+        per_step = a.global_batch
+        begin, end = shard.shard_range(per_step, world, rank)
+        n_r = end - begin
+        if n_r < 1:
+            raise SystemExit(f"global batch {per_step} < {world} ranks")
+        first = lambda j: j * max(1, per_step // a.batch) + begin // a.batch
+    B = a.batch if n_r % a.batch == 0 and (weak or begin % a.batch == 0) else n_r
+    G = n_r // B  # independent batches per call (DPFT_GROUP)
+    slot_inputs = [make_batches(B, first(j), G, device, a.icp) for j in range(S)]
     sel, levels_nchw, K = slot_inputs[0]
 
     def packed(levels):
         return [dict(d, x0=ic.pack_features(d["x0"]), x1=ic.pack_features(d["x1"])) for d in levels]
 
-    def pack_time_us(levels, reps=10):
-        """One-time NCHW -> channel-quad conversion of both feature pyramids (not in the step)."""
-        packed(levels)
-        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-        e0.record()
-        for _ in range(reps):
-            packed(levels)
-        e1.record()
+    pose_init = torch.cat((torch.eye(3, device=device).repeat(n_r, 1, 1).reshape(-1),
+                           torch.zeros(n_r * 3, device=device)))
+
+    def capture(fn):
+        fn()
         torch.cuda.synchronize()
-        return e0.elapsed_time(e1) / reps * 1e3
+        if a.no_graph:
+            return fn
+        s = torch.cuda.Stream(device)
+        s.wait_stream(torch.cuda.current_stream(device))
+        with torch.cuda.stream(s):
+            fn()
+        torch.cuda.current_stream(device).wait_stream(s)
+        graph = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(graph):
+            fn()
+        torch.cuda.synchronize()
+        return graph.replay
 
-    levels = packed(levels_nchw) if a.layout == "c4" else levels_nchw
-    # R [B,3,3] and t [B,3] as two contiguous views of one buffer: one reset copy per step
-    pose_init = torch.cat((torch.eye(3, device=device).repeat(BG, 1, 1).reshape(-1), torch.zeros(BG * 3, device=device)))
-
-    def make_step(levels, K=K):
-        solver = ic.PyramidSolver(levels, K, iters=ITERS, remove_tru_sigma=True, group=B,
-                                  schedule=os.environ.get("DPFT_BENCH_SCHEDULE"))  # A/B only
+    def make_step(levels, K, pre=None):
+        solver = ic.PyramidSolver(levels, K, iters=ITERS, remove_tru_sigma=True, combine_icp=a.icp,
+                                  group=B if G > 1 else None)
         pose = pose_init.clone()
-        R, t = pose[:9 * BG].view(BG, 3, 3), pose[9 * BG:].view(BG, 3)
+        R, t = pose[:9 * n_r].view(n_r, 3, 3), pose[9 * n_r:].view(n_r, 3)
 
         def solve():
+            if pre is not None:
+                pre()
             pose.copy_(pose_init)
             solver.run(R, t)
-
-        # eager warm-up (also validates), then capture the whole 4-level solve into one graph
         solve()
         torch.cuda.synchronize()
         ic.check_status(solver.status)
-        graph = None
-        if not a.no_graph:
-            s = torch.cuda.Stream(device)
-            s.wait_stream(torch.cuda.current_stream(device))
-            with torch.cuda.stream(s):
-                solve()
-            torch.cuda.current_stream(device).wait_stream(s)
-            graph = torch.cuda.CUDAGraph()
-            with torch.cuda.graph(graph):
-                solve()
-            torch.cuda.synchronize()
+        return solver, R, t, capture(solve)
 
-        def run():
-            if graph is not None:
-                graph.replay()
-            else:
-                solve()
-        return solver, R, t, run, graph is not None
-
-    # S in-flight slots: slot j solves its own batch on its own stream from its own HIP
-    # graph and workspace; step k runs on slot k % S, so a batch's latency-bound coarse
-    # levels and finalizes overlap another batch's bandwidth-bound level 0
-    slots = []
-    for j in range(S):
-        lv = levels if j == 0 else (packed(slot_inputs[j][1]) if a.layout == "c4" else slot_inputs[j][1])
-        slots.append(make_step(lv, slot_inputs[j][2]))
+    slot_levels = [packed(si[1]) if a.layout == "c4" else si[1] for si in slot_inputs]
+    slots = [make_step(slot_levels[j], slot_inputs[j][2]) for j in range(S)]
     streams = [torch.cuda.Stream(device) for _ in range(S)]
-    solver, R, t, run, graphed = slots[0]
-    # N > 1: the pose gather of step k runs on the collective stream while step k + 1
-    # solves (double-buffered output; poses packed into a fresh buffer first, on the
-    # slot's stream); every gather is waited for inside the timed region (drain())
-    gathered = [torch.empty(world * BG, 12, device=device) for _ in range(2)] if world > 1 else None
+    solver, R, t, run = slots[0]
+    gathered = [torch.empty(world * n_r, 12, device=device) for _ in range(2)] if world > 1 else None
     pending = [None]
-    nstep = [0]
 
     def drain():
         if pending[0] is not None:
             pending[0].wait()
             pending[0] = None
 
-    def step():
-        j = nstep[0] % S
-        with torch.cuda.stream(streams[j]):
-            slots[j][3]()
-            if world > 1:
-                drain()
-                _, pending[0] = shard.gather_poses(slots[j][1], slots[j][2], out=gathered[nstep[0] % 2],
-                                                   async_op=True)
-        nstep[0] += 1
-
     def barrier():
         if world > 1:
             import torch.distributed as dist
             dist.barrier()
 
-    # setup warm-up by wall time (untimed, before the W warm-up steps): a few ms of load
-    # leave the chip below its steady clock (MI355X_MICROARCH.md, DVFS) -- measured 141 k
-    # vs 150 k IC iterations/s for 20 timed steps after 5 vs 300 warm-up steps.  Solves
-    # only, no pose gathers: the ranks run different numbers of these rounds, and a
-    # collective issued by one rank and not the other would deadlock.
-    torch.cuda.synchronize()
-    tw = time.perf_counter()
-    while time.perf_counter() - tw < a.setup_warm_ms * 1e-3:
-        for j in range(S):
+    def timed_loop(slots, steps, warmup):
+        """W warm-up then K timed steps (step k on slot k % S), barrier + synchronize on both
+        sides; the N > 1 pose gather of step k overlaps step k + 1 (double-buffered)."""
+        nstep = [0]
+
+        def step():
+            j = nstep[0] % len(slots)
             with torch.cuda.stream(streams[j]):
                 slots[j][3]()
+                if world > 1:
+                    drain()
+                    _, pending[0] = shard.gather_poses(slots[j][1], slots[j][2], out=gathered[nstep[0] % 2],
+                                                       async_op=True)
+            nstep[0] += 1
+        # setup warm-up by wall time, solves only (no collective: ranks run different counts)
         torch.cuda.synchronize()
-    for _ in range(a.warmup):
-        step()
-    drain()
-    torch.cuda.synchronize()
-    barrier()
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    for _ in range(a.steps):
-        step()
-    drain()
-    torch.cuda.synchronize()
-    barrier()
-    torch.cuda.synchronize()
-    elapsed = time.perf_counter() - t0
-    if world > 1:
-        import torch.distributed as dist
-        e = torch.tensor([elapsed], device=device, dtype=torch.float64)
-        dist.all_reduce(e, op=dist.ReduceOp.MAX)
-        elapsed = e.item()
+        tw = time.perf_counter()
+        while time.perf_counter() - tw < a.setup_warm_ms * 1e-3:
+            for j, sl in enumerate(slots):
+                with torch.cuda.stream(streams[j]):
+                    sl[3]()
+            torch.cuda.synchronize()
+        for _ in range(warmup):
+            step()
+        drain()
+        torch.cuda.synchronize()
+        barrier()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(steps):
+            step()
+        drain()
+        torch.cuda.synchronize()
+        barrier()
+        torch.cuda.synchronize()
+        el = time.perf_counter() - t0
+        if world > 1:
+            import torch.distributed as dist
+            e = torch.tensor([el], device=device, dtype=torch.float64)
+            dist.all_reduce(e, op=dist.ReduceOp.MAX)
+            el = e.item()
+        return el
+
+    log(f"rank {rank}: {n_r} pairs per step in {G} batch(es) of {B}, {S} in flight; timing {a.steps} steps")
+    elapsed = timed_loop(slots, a.steps, a.warmup)
+    log(f"rank {rank}: {elapsed / a.steps * 1e3:.3f} ms per step")
     for sl in slots:
         ic.check_status(sl[0].status)
     ms_per_step = elapsed / a.steps * 1e3
-    iters_total = world * BG * LEVELS * ITERS * a.steps
-    value = iters_total / elapsed
-    # latency of one solve (slot 0 alone, back to back on one stream), rank 0 only
+    value = per_step * LEVELS * ITERS * a.steps / elapsed
+
+    # end-to-end from the reference's NCHW layout: the step also packs both frames' feature
+    # pyramids into the channel-quad buffers the solve reads (every pair packs its own two
+    # frames), captured in the same graph; same timed loop (rank 0 and all ranks alike)
+    e2e = None
+    if a.layout == "c4" and not a.no_compare:
+        def packer(src, dst):
+            L = ic.N.lib()
+
+            def pk():
+                for l in range(LEVELS):
+                    for key in ("x0", "x1"):
+                        s_, d_ = src[l][key], dst[l][key]
+                        ic.N.check(L.dpft_pack_features(ic._ptr(s_), ic._ptr(d_), s_.shape[0], C, s_.shape[2],
+                                                        s_.shape[3], ic._stream(device)), "dpft_pack_features")
+            return pk
+        e2e_slots = [make_step(slot_levels[j], slot_inputs[j][2], pre=packer(slot_inputs[j][1], slot_levels[j]))
+                     for j in range(S)]
+        el = timed_loop(e2e_slots, a.steps, a.warmup)
+        e2e = {"value": per_step * LEVELS * ITERS * a.steps / el, "ms_per_step": el / a.steps * 1e3,
+               "what": "each step also converts both frames' NCHW feature pyramids (x0, x1, 4 levels, every pair) "
+                       "to the channel-quad layout (dpft_pack_features) inside the timed graph"}
+        del e2e_slots
+
+    # latency of one step alone (slot 0, back to back on one stream), rank 0 only
     latency_ms = None
     if rank == 0:
         n_lat = min(a.steps, 50)
-        torch.cuda.synchronize()
-        tl0 = time.perf_counter()
-        for _ in range(n_lat):
-            run()
-        torch.cuda.synchronize()
-        latency_ms = (time.perf_counter() - tl0) / n_lat * 1e3
+        latency_ms = _timed(run, n_lat, device) * 1e3
 
-    # ---- roofline of the dominant kernel: the level-0 fused reduce (+ its in-kernel
-    # finalize), i.e. exactly the launches the solve makes at level 0 -- iterations
-    # forward, reverse, forward (DPFT_ITER_REVERSE), the group repeated -- continuing
-    # from the solved pose; timed with HIP events on the stream they are launched on
-    # (the current stream).
+    # ---- roofline of the dominant kernel: the level-0 fused reduce (+ in-kernel finalize),
+    # exactly the launches the solve makes at level 0 (iterations forward, reverse, forward
+    # -- DPFT_ITER_REVERSE -- continuing from the solved pose), HIP events on the stream they
+    # are launched on (the current stream)
     Rk, tk = R.clone(), t.clone()
     solver.iterate(0, Rk, tk, first=True)
     l0_group = [False, True, False]
     for rev in l0_group:
         solver.iterate(0, Rk, tk, reverse=rev)
     groups = max(1, a.kernel_reps // len(l0_group))
-    ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-    ev0.record()
-    for _ in range(groups):
+
+    def l0():
         for rev in l0_group:
             solver.iterate(0, Rk, tk, reverse=rev)
-    ev1.record()
-    torch.cuda.synchronize()
-    kern_us = ev0.elapsed_time(ev1) / (groups * len(l0_group)) * 1e3
+    kern_us = _timed(l0, groups, device) / len(l0_group) * 1e6
     alg_bytes = solver.algorithmic_bytes(0)
     achieved = alg_bytes / (kern_us * 1e-6) / 1e9
-    traffic = l0_traffic(BG, B) if a.layout == "c4" else None
+    mode = 1 if a.icp else 0
+    kname = f"_ZN12_GLOBAL__N_116ic_reduce_kernelILi32ELb1ELb1ELi{mode}ELb1EEEvNS_10IterParamsE"
+    traffic = l0_traffic(n_r, B, kname) if a.layout == "c4" else None
     copy_gbs = copy_peak_gbs(device) if rank == 0 else None
     read_gbs = read_peak_gbs(device, alg_bytes) if rank == 0 else None
 
-    # secondary (rank 0 only, not the headline): the same solve from the other resident
-    # layout, and the one-time cost of packing NCHW pyramids into the channel-quad layout
     other = None
     if rank == 0 and not a.no_compare:
         other_layout = "nchw" if a.layout == "c4" else "c4"
-        o_solver, o_R, o_t, o_run, _ = make_step(levels_nchw if other_layout == "nchw" else packed(levels_nchw))
+        o_solver, o_R, o_t, o_run = make_step(levels_nchw if other_layout == "nchw" else packed(levels_nchw), K)
         for _ in range(a.warmup):
             o_run()
-        torch.cuda.synchronize()
-        tt0 = time.perf_counter()
-        for _ in range(a.steps):
-            o_run()
-        torch.cuda.synchronize()
-        o_el = time.perf_counter() - tt0
-        dpose = max((o_R - R).abs().max().item(), (o_t - t).abs().max().item())
-        other = {"layout": other_layout, "ms_per_step": o_el / a.steps * 1e3,
-                 "value": BG * LEVELS * ITERS * a.steps / o_el, "max_abs_pose_diff_vs_headline": dpose,
-                 "pack_us_all_levels_both_frames": pack_time_us(levels_nchw)}
+        sec = _timed(o_run, a.steps, device)
+        other = {"layout": other_layout, "ms_per_step_sequential": sec * 1e3,
+                 "value_sequential": n_r * LEVELS * ITERS / sec,
+                 "max_abs_pose_diff_vs_headline": max((o_R - R).abs().max().item(), (o_t - t).abs().max().item())}
         del o_solver
 
     cpu = None
     if rank == 0 and world == 1 and not a.no_cpu_baseline:
-        best, dR, dt, epe, one_thread, rpe_trs = cpu_baseline(levels_nchw, K, R, t)
-        cpu = {"value": LEVELS * ITERS / best, "unit": "IC iterations/s",
-               "cores": torch.get_num_threads(), "kind": "port", "cpu_model": cpu_model(),
-               "value_1_thread": LEVELS * ITERS / one_thread, "seconds_per_pair_1_thread": one_thread,
-               "sample": "1 pair, 640x480 C=32, 4 levels x 3 iters, oracle/ic_oracle.py (PyTorch-CPU fp32 "
-                         "restatement of algorithms.py:611-723), best of 2 after 1 warm-up",
-               "seconds_per_pair": best, "gpu_vs_oracle_max_abs_dR": dR, "gpu_vs_oracle_max_abs_dt": dt,
-               "gpu_vs_oracle_3dpe_m": epe, "gpu_vs_oracle_rpe_trans_m": rpe_trs}
+        log(f"CPU baseline: the oracle on batch 0 ({B} pairs) at {host_cpus()} threads, then one pair on one thread")
+        cpu = cpu_baseline(levels_nchw, K, R, t, B, a.icp)
 
     if rank == 0:
+        bpa = 280 if a.icp else 272
         line = {
-            "metric": "IC solver iters/sec (640x480, C=32, 4-level)",
+            "metric": "IC solver iters/sec (640x480, C=32, 4-level)" + (" + combine_ICP" if a.icp else ""),
             "value": value, "unit": "IC iterations/s (all levels, 12 per pair)",
             "n_gpus": world, "steps": a.steps, "warmup": a.warmup, "ms_per_step": ms_per_step,
-            "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "f32",
-            "data": "synthetic: deterministic triangle-wave features of the 5 TUM fr1/desk example frames",
-            "config": {"workload": "cfg2/cfg3 shard: 640x480, C=32, Cs=1, 4 levels x 3 GN iters, "
-                                   "remove_tru_sigma, batches of B pairs per GPU", "pairs_per_gpu": B,
-                       "global_batch": world * B, "parallelism": f"pair-sharded x{world}, RCCL all-gather of poses",
-                       "graph": graphed, "feature_layout": a.layout,
-                       "batches_per_launch": G, "pairs_per_launch": BG, "inflight": S,
-                       "setup_warm_ms": a.setup_warm_ms},
-            "latency_ms_per_solve": latency_ms,
-            "pairs_per_s": world * BG * a.steps / elapsed,
-            "l0_iters_per_s": world * BG * ITERS * a.steps / elapsed,
+            "higher_is_better": True, "scaling": "weak" if weak else "strong", "vs_baseline": None, "dtype": "f32",
+            "data": "synthetic: deterministic triangle-wave features of the 5 TUM fr1/desk example frames "
+                    "(tests/golden/recipe.py; trained checkpoints absent)",
+            "config": {"workload": ("cfg5: " if a.icp else "cfg3: ") +
+                                   ("eval stream of global batches of %d pairs, " % per_step if not weak else
+                                    "weak scaling, %d pairs per GPU per step, " % n_r) +
+                                   "640x480, C=32, Cs=1, 4 levels x 3 GN iters, remove_tru_sigma" +
+                                   (", combine_ICP (w=0.01)" if a.icp else ""),
+                       "global_batch": per_step, "pairs_per_gpu": n_r, "batch": B, "batches_per_launch": G,
+                       "pairs_per_launch": n_r, "inflight": S,
+                       "parallelism": f"pair-sharded x{world}, RCCL all-gather of poses",
+                       "graph": not a.no_graph, "feature_layout": a.layout, "setup_warm_ms": a.setup_warm_ms},
+            "latency_ms_per_step": latency_ms,
+            "pairs_per_s": per_step * a.steps / elapsed,
+            "l0_iters_per_s": per_step * ITERS * a.steps / elapsed,
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": achieved / HBM_PEAK_GBS,
                          "traffic": traffic["hbm_bytes"] if traffic else None,
                          "traffic_source": traffic["source"] if traffic else None,
-                         "kernel": f"ic_reduce_kernel<32,Cs=1,tru,U_IC,{a.layout}> (level 0, + in-kernel finalize)",
+                         "kernel": f"ic_reduce_kernel<32,Cs=1,tru,{'U_IC+ICP' if a.icp else 'U_IC'},{a.layout}> "
+                                   f"(level 0, {n_r} pairs per launch, + in-kernel finalize)",
                          "kernel_us": kern_us, "algorithmic_bytes_per_launch": alg_bytes,
+                         "algorithmic_bytes_per_pixel": bpa,
                          "measured_copy_peak": copy_gbs,
                          "frac_of_measured_copy_peak": achieved / copy_gbs if copy_gbs else None,
                          "measured_read_peak": read_gbs,
                          "frac_of_measured_read_peak": achieved / read_gbs if read_gbs else None},
+            "end_to_end_from_nchw": e2e,
             "cpu_baseline": cpu,
             "other_layout": other,
         }

@@ -21,7 +21,7 @@ FEATURES_C4 = 0x8
 SCHEDULES = {"auto": 0x00, "march": 0x10, "split": 0x20}  # DPFT_SCHED_*
 EXT_SLOT_SHIFT = 12       # DPFT_EXT_SLOT(k) = (k + 1) << 12
 EXTREMA_READY = 0x10000
-GROUP_SHIFT = 20          # DPFT_GROUP(n) = n << 20: n pairs per independent batch (bits 20-27)
+GROUP_SHIFT = 20          # DPFT_GROUP(n) = n << 20: n pairs per independent batch (bits 20-31)
 GROUP_MAX_BATCHES = 32
 STATUS_NONFINITE = 0x1
 ABI_VERSION = 2
@@ -49,7 +49,7 @@ EXPORTS = ("dpft_workspace_size", "dpft_ic_solve_level", "dpft_ic_solve_pyramid"
            "dpft_ic_reduce_only", "dpft_ic_debug_pixels", "dpft_preprocess_workspace_size",
            "dpft_preprocess_depth", "dpft_pack_features", "dpft_pack_features_nhwc", "dpft_bn_elu", "dpft_sigma_extrema_levels", "dpft_ic_damped_update", "dpft_feature_gradient", "dpft_warp_jacobian",
            "dpft_inverse_jacobian", "dpft_normal_equations_workspace_size", "dpft_normal_equations",
-           "dpft_read_probe_out_floats", "dpft_read_probe", "dpft_version", "dpft_last_error")
+           "dpft_read_probe_out_floats", "dpft_read_probe", "dpft_copy_probe", "dpft_version", "dpft_last_error")
 
 _lib = None
 
@@ -114,6 +114,8 @@ def lib():
     L.dpft_read_probe_out_floats.restype = sz
     L.dpft_read_probe.argtypes = [vp, sz, ctypes.c_int32, vp, vp]
     L.dpft_read_probe.restype = ctypes.c_int
+    L.dpft_copy_probe.argtypes = [vp, vp, sz, ctypes.c_int32, vp]
+    L.dpft_copy_probe.restype = ctypes.c_int
     L.dpft_version.argtypes = []
     L.dpft_version.restype = ctypes.c_int
     L.dpft_last_error.argtypes = []

@@ -95,17 +95,26 @@ def isa_hashes(so_path=OUT):
 
 
 def write_isa_hashes():
+    """Best effort: the hashes only let bench.py match a committed PMC measurement to the
+    kernel built here; a missing LLVM tool must not make the library unusable."""
     import json
-    json.dump(isa_hashes(OUT), open(ISA_OUT, "w"), indent=0, sort_keys=True)
+    import warnings
+    try:
+        json.dump(isa_hashes(OUT), open(ISA_OUT, "w"), indent=0, sort_keys=True)
+    except (OSError, subprocess.CalledProcessError) as e:
+        warnings.warn(f"ISA hashes not written ({e}); bench.py will report roofline.traffic = null")
 
 
 def build(force=False, verbose=False):
-    deps = [SRC, os.path.join(INC, "dpft_ic.h"), __file__]
+    deps = [SRC, os.path.join(HERE, "csrc", "dpft_tuning.h"), os.path.join(INC, "dpft_ic.h"), __file__]
     if not force and os.path.exists(OUT) and os.path.getmtime(OUT) >= max(os.path.getmtime(d) for d in deps):
         if not os.path.exists(ISA_OUT) or os.path.getmtime(ISA_OUT) < os.path.getmtime(OUT):
             write_isa_hashes()
         return OUT
+    # -Wshadow: a local that shadows a buffer resource of the marching body compiles to a
+    # silently wrong kernel (round 2: `rs0`, JtJ off by 1e8); every warning is an error
     cmd = [HIPCC, f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-shared", "-fPIC", f"-I{INC}",
+           "-Wall", "-Wextra", "-Wshadow", "-Werror",
            "-Rpass-analysis=kernel-resource-usage", "-o", OUT + ".tmp", SRC]
     if verbose:
         print(" ".join(cmd), file=sys.stderr)

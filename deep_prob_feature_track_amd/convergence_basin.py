@@ -172,3 +172,69 @@ def convergence_counts(R_est, t_est, R_gt, t_gt, rot_thresh=0.01, trans_thresh=0
     return int(ok.sum().item()), {'rot_margin': (rot_thresh - ae).cpu().numpy(),
                                   'trans_margin': (trans_thresh - te).cpu().numpy(),
                                   'converged': ok.cpu().numpy()}
+
+
+# ---------------------------------------------------------------------------------------
+# Solves from perturbed starts (cfg4: the large-baseline convergence-basin sweep)
+#
+# The reference's LeastSquareTracking.forward has no initial-pose argument; a solve from a
+# given start is the per-level solver chain tr_update3 .. tr_update0 entered with that pose
+# (LeastSquareTracking.py:349-445 after the init pose of 686-695), which is what
+# ic.PyramidSolver runs.  Each start set (one start per pair) is solved as its own
+# reference call over the batch -- its own batch-global truncated-sigma extrema -- and up
+# to 32 start sets share every launch as independent batches (DPFT_GROUP).
+
+def solve_from_starts(levels, K, R0, t0, iters=3, remove_tru_sigma=True, max_pairs=2048):
+    """levels: per-level dicts of B pairs (x0, x1 NCHW or channel-quad packed, invD0, invD1,
+    sigma0, sigma1[, obj_mask0, obj_mask1]), K [B,4] level-0 intrinsics; R0 [P,B,3,3],
+    t0 [P,B,3(,1)] start poses -> (R [P,B,3,3], t [P,B,3]): start set p solved as one call
+    over the B pairs.  Start sets go max_pairs // B at a time (at most 32) through one
+    grouped PyramidSolver; a short last round is padded with copies of its first set."""
+    from . import _native as N
+    from . import ic
+    P, B = R0.shape[:2]
+    if B > max_pairs:
+        raise ValueError(f"B={B} pairs exceed {max_pairs} per call")
+    G = max(1, min(P, N.GROUP_MAX_BATCHES, max_pairs // B))
+    rep = lambda v: v.repeat(G, *([1] * (v.dim() - 1))) if G > 1 else v
+    lv = [{k: rep(v) for k, v in d.items()} for d in levels]
+    solver = ic.PyramidSolver(lv, rep(K.reshape(B, 4)).contiguous(), iters=iters, remove_tru_sigma=remove_tru_sigma,
+                              group=B if G > 1 else None)
+    dev = levels[0]["x0"].device
+    R0 = R0.to(device=dev, dtype=torch.float32).reshape(P, B, 3, 3)
+    t0 = t0.to(device=dev, dtype=torch.float32).reshape(P, B, 3)
+    R = torch.empty(G * B, 3, 3, device=dev)
+    t = torch.empty(G * B, 3, device=dev)
+    out_R, out_t = torch.empty(P, B, 3, 3, device=dev), torch.empty(P, B, 3, device=dev)
+    for p0 in range(0, P, G):
+        g = min(G, P - p0)
+        idx = list(range(p0, p0 + g)) + [p0] * (G - g)
+        R.copy_(R0[idx].reshape(G * B, 3, 3))
+        t.copy_(t0[idx].reshape(G * B, 3))
+        solver.run(R, t)
+        out_R[p0:p0 + g] = R[:g * B].view(g, B, 3, 3)
+        out_t[p0:p0 + g] = t[:g * B].view(g, B, 3)
+    ic.check_status(solver.status)
+    return out_R, out_t
+
+
+def perturbed_starts(R_c, t_c, rot_pert, trs_pert):
+    """Start poses [6 S, B] around the pose (R_c, t_c): the reference's 1-D sweep axes
+    (convergence_basin.py:337-418: static x-y-z Euler offsets for rotation, offsets of one
+    translation coordinate) applied as initial poses instead of residual evaluations."""
+    return axis_perturbations(R_c, t_c.reshape(-1, 3), rot_pert, trs_pert)
+
+
+def basin_counts(R_fin, t_fin, R_tgt, t_tgt, rot_thresh=0.01, trans_thresh=0.01):
+    """Convergence of every start set: count [P] of pairs whose solve from that start lands
+    within (rot_thresh rad, trans_thresh m) of the target pose (compute_RPE_loss errors),
+    and the per-(start, pair) margins [P,B] (threshold - error; a count is stable under a
+    pose noise eps when no |margin| is below it)."""
+    P, B = R_fin.shape[:2]
+    counts, rot_m, trs_m = [], [], []
+    for p in range(P):
+        n, m = convergence_counts(R_fin[p], t_fin[p], R_tgt, t_tgt, rot_thresh, trans_thresh)
+        counts.append(n)
+        rot_m.append(m["rot_margin"])
+        trs_m.append(m["trans_margin"])
+    return np.array(counts), {"rot_margin": np.stack(rot_m), "trans_margin": np.stack(trs_m)}

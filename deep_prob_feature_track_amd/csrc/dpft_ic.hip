@@ -53,6 +53,7 @@
 #include <vector>
 
 #include "dpft_ic.h"
+#include "dpft_tuning.h"
 
 // LLVM buffer-load intrinsics (declared at global scope: they bind by asm label).
 typedef int Rsrc __attribute__((ext_vector_type(4)));
@@ -67,113 +68,21 @@ namespace {
 constexpr int kThreads = 256;          // 4 waves of 64
 constexpr int kTileW = 64;             // one wave = 64 consecutive pixels of a row
 constexpr int kRowsPerStep = 4;        // one row per wave per step
-#ifndef DPFT_RING
-#define DPFT_RING 2
-#endif
-#ifndef DPFT_RPL
-#define DPFT_RPL 1
-#endif
-#ifndef DPFT_ROWMAJOR
-#define DPFT_ROWMAJOR 0
-#endif
-#ifndef DPFT_ABL
-#define DPFT_ABL 0  // ablation builds for profiling only (1: no channel loop, 2: channel loads only)
-#endif
-#ifndef DPFT_RPL4
-#define DPFT_RPL4 1
-#endif
-#ifndef DPFT_CK
-#define DPFT_CK 2
-#endif
-#ifndef DPFT_MAX_STEPS
-#define DPFT_MAX_STEPS 4
-#endif
-#ifndef DPFT_MIN_WAVES
-#define DPFT_MIN_WAVES 1  // (2 pins <= 256 VGPRs but schedules the marching loop 4-5 % slower; build.py checks instead)
-#endif
-#ifndef DPFT_MARCH
-#define DPFT_MARCH 1
-#endif
-#ifndef DPFT_RING_M
-#define DPFT_RING_M 2
-#endif
-constexpr bool kMarch = DPFT_MARCH != 0;  // channel-quad reduce: row-marching window (1) or 4-row tiles (0)
-#ifndef DPFT_SPLIT_MAX_PIXELS
-#define DPFT_SPLIT_MAX_PIXELS 40000
-#endif
-constexpr long kSplitMaxPixels = DPFT_SPLIT_MAX_PIXELS;  // channel-quad levels up to this size per pair: ic_split_kernel
-#ifndef DPFT_SPLIT_MAX_LAUNCH_PIXELS
-#define DPFT_SPLIT_MAX_LAUNCH_PIXELS 320000
-#endif
-// ... and up to this many pixels per launch (all pairs): a level of a grouped call
-// (DPFT_GROUP) with more fills the device as a marching launch (level 2 of 32 pairs:
-// 614 k pixels, the size of level 1 of 8 pairs, where marching is the faster schedule)
+constexpr int kRing = 2;               // tile paths: load slots in flight (kRing - 1 units ahead)
+constexpr int kCK = 2;                 // tile paths, NCHW: channels per pipeline unit
+constexpr int kRPL = 1;                // image rows per lane (one sigma plane, NCHW)
+constexpr int kRPL4 = 1;               // image rows per lane (channel-quad tile path)
+constexpr int kMaxSteps = 4;           // tile paths: up to 4 * kMaxSteps rows per workgroup
+// channel-quad levels of at most kSplitMaxPixels per pair (and kSplitMaxLaunchPixels per
+// launch, all pairs): ic_split_kernel; larger ones march (a level of a grouped call with
+// more -- level 2 of 32 pairs: 614 k pixels, the size of level 1 of 8 pairs -- fills the
+// device as a marching launch)
+constexpr long kSplitMaxPixels = DPFT_SPLIT_MAX_PIXELS;
 constexpr long kSplitMaxLaunchPixels = DPFT_SPLIT_MAX_LAUNCH_PIXELS;
-#ifndef DPFT_SPLIT_SEPFIN
-#define DPFT_SPLIT_SEPFIN 1
-#endif
-constexpr bool kSplitSepFin = DPFT_SPLIT_SEPFIN != 0;
-#ifndef DPFT_SEPFIN_MAX_PIXELS
-#define DPFT_SEPFIN_MAX_PIXELS 0
-#endif
-constexpr long kSepFinMaxPixels = DPFT_SEPFIN_MAX_PIXELS;  // ic_reduce_kernel levels finalized by a separate launch
-#ifndef DPFT_MARCH_ROWS
-#define DPFT_MARCH_ROWS 1
-#endif
-#ifndef DPFT_MARCH_CSPLIT
-#define DPFT_MARCH_CSPLIT 1
-#endif
-constexpr int kMarchCSplit = DPFT_MARCH_CSPLIT;  // waves sharing a marching band (channel quads split)
-#ifndef DPFT_MARCH_REVERSE
-#define DPFT_MARCH_REVERSE 1
-#endif
-constexpr bool kMarchReverse = DPFT_MARCH_REVERSE != 0;  // honour DPFT_ITER_REVERSE
-#ifndef DPFT_MARCH_SKEW
-#define DPFT_MARCH_SKEW 10
-#endif
 constexpr int kMarchSkew = DPFT_MARCH_SKEW;  // band-size skew of the marching schedule (64ths, 0..63)
-#ifndef DPFT_MARCH_GRID
-#define DPFT_MARCH_GRID 1
-#endif
-// marching bands on a (row band x strip) grid: every strip cut at the same rows, so the
-// waves of horizontally adjacent strips read their shared columns at the same time
-constexpr bool kMarchGrid = DPFT_MARCH_GRID != 0;
-#ifndef DPFT_MARCH_HYBRID
-#define DPFT_MARCH_HYBRID 1
-#endif
-// S < waves < 2 S per pair (level 0 of a 128-pair launch: 16 waves over 11 strips): wave
-// s < S marches the top rows of strip s (common row cuts per weight class), the other
-// waves split the strips' bottom rows strip-major
-constexpr bool kMarchHybrid = DPFT_MARCH_HYBRID != 0;
-constexpr int kMarchRows = DPFT_MARCH_ROWS;  // rows per marching step (1, or 2: -10 % f1 traffic, +11 % VALU, 4 % slower)
-constexpr int kRingM = DPFT_RING_M;       // quads in flight on the marching path (kRingM - 1 ahead)
-#ifndef DPFT_UNROLL_Q
-#define DPFT_UNROLL_Q 1  // marching path: the quad loop straight-line (static quad indices)
-#endif
-#ifndef DPFT_RING_Q
-#define DPFT_RING_Q 4
-#endif
-constexpr int kRingQ = DPFT_RING_Q;  // straight-line marching quad loop: quads in flight
-#ifndef DPFT_LATE_TERMS
-#define DPFT_LATE_TERMS 0
-#endif
-constexpr bool kLateTerms = DPFT_LATE_TERMS != 0;  // pixel terms after the channel loop
-#ifndef DPFT_TAP_CACHE
-#define DPFT_TAP_CACHE 1
-#endif
-// marching path: keep the leading f1 tap pair of every quad in registers for the next row
-constexpr bool kTapCache = DPFT_TAP_CACHE != 0 && DPFT_UNROLL_Q != 0 && DPFT_MARCH_ROWS == 1 && DPFT_ABL == 0;
-#ifndef DPFT_F0_AUX
-#define DPFT_F0_AUX 2
-#endif
-constexpr int kF0Aux = DPFT_F0_AUX;       // cache policy of the marching f0 stream (2: nt)
-constexpr int kCK = DPFT_CK;           // channels per pipeline unit
-constexpr int kRing = DPFT_RING;       // load slots in flight ring (kRing - 1 units ahead)
-constexpr int kRPL = DPFT_RPL;         // image rows per lane (Cs == 1 kernels)
-constexpr int kRPL4 = DPFT_RPL4;       // image rows per lane (channel-quad layout)
-constexpr int kLdsW = kTileW + 2;      // 1-pixel halo each side
-constexpr int kLdsH = kRowsPerStep + 2;
-constexpr int kMaxSteps = DPFT_MAX_STEPS;  // up to 4 * kMaxSteps rows per workgroup
+constexpr int kRingQ = DPFT_RING_Q;          // marching quad loop: quads in flight (kRingQ - 1 ahead)
+constexpr int kF0Aux = 2;                    // cache policy of the marching f0 stream (nt: used once)
+constexpr int kGridWaste = 4;                // marching band grid: idle waves allowed (64ths of a pair's)
 
 // ---- reduce-record layout (floats) ------------------------------------------
 constexpr int kRec = 48;
@@ -198,26 +107,18 @@ constexpr int L_SUM = 0, L_NINV = 1, L_MN_ALL = 2, L_MN0 = 3, L_LMN = 4, L_NMN =
 // kCtlMMDoneL / kCtlExtSlots: dpft_sigma_extrema_levels' per-level completion counters and
 // the per-level sigma0 extrema it leaves (DPFT_EXT_SLOT / DPFT_EXTREMA_READY)
 constexpr int kCtlMMDoneL = 10, kCtlExtSlots = 16, kMaxExtSlots = 8;
-constexpr int kCtlMin = 0, kCtlMax = 1, kCtlDone = 2, kCtlMMDone = 3, kCtlResDone = 4, kCtlD1Min = 8,
+constexpr int kCtlMin = 0, kCtlMax = 1, kCtlDone = 2, kCtlMMDone = 3, kCtlD1Min = 8,
               kCtlPart = 64, kCtlPair = 1152;
 constexpr int kMaxMMBlocks = 512;
 // pair_reduce2's LDS scratch: 42 fields x 65 quad rows (the extrema exchange overlaps it)
 constexpr int kFinScratch = 42 * 65;
 // cache-policy operand of the raw buffer intrinsics: sc1 (agent-coherent; gfx940+ bit 4)
 constexpr int kAuxSc1 = 16;
-// DPFT_TAIL_PROF builds only: per-workgroup finish stamps, per-pair reduce stamps, batch stamps
-constexpr int kCtlTail = 3264, kTailWG = 768, kTailPairs = 16;
-#ifndef DPFT_MM_GRID
-#define DPFT_MM_GRID 128
-#endif
-#ifndef DPFT_MM_LOADS
-#define DPFT_MM_LOADS 8
-#endif
 // minmax_kernel: workgroups (<= kMaxMMBlocks) and 16-byte loads in flight per thread.
 // Its last-workgroup reduction serialises one counter arrival per workgroup.
 constexpr int kMMGrid = DPFT_MM_GRID, kMMLoads = DPFT_MM_LOADS;
 static_assert(kMMGrid <= kMaxMMBlocks, "minmax partials");
-static_assert(DPFT_MARCH_SKEW >= 0 && DPFT_MARCH_SKEW < 64, "band skew in 64ths");
+static_assert(kMarchSkew >= 0 && kMarchSkew < 64, "band skew in 64ths");
 constexpr int kMaxPairs = 2048;  // per call (one completion counter per pair)
 constexpr int kMaxGrid = 4096;   // reduce-kernel workgroups (resident capacity is far below)
 // Independent batches in one call (DPFT_GROUP): per batch a completion counter of the
@@ -225,12 +126,14 @@ constexpr int kMaxGrid = 4096;   // reduce-kernel workgroups (resident capacity 
 // kMaxExtSlots = a call without DPFT_EXT_SLOT) and the pre-pass counters per (level, batch).
 constexpr int kMaxGroups = 32;
 constexpr int kCtlGDone = 32, kCtlGExt = 4096, kCtlGMMDone = kCtlGExt + 2 * (kMaxExtSlots + 1) * kMaxGroups;
+// combine_ICP: depth1 extrema per independent batch (the normal map's invalid-depth test)
+constexpr int kCtlGD1 = kCtlGMMDone + 4 * kMaxGroups;
 constexpr size_t kCtrlBytes = 20480;
+static_assert((kCtlGD1 + 2 * kMaxGroups) * 4 <= kCtrlBytes, "ctrl area (batch depth extrema)");
 static_assert(kCtlGDone + kMaxGroups <= kCtlPart, "batch counters");
 static_assert((kCtlGMMDone + 4 * kMaxGroups) * 4 <= kCtrlBytes, "ctrl area (batches)");
 static_assert((kCtlPart + 2 * kMaxMMBlocks) * 4 <= kCtlPair * 4, "ctrl area");
 static_assert((kCtlPair + kMaxPairs) * 4 <= kCtrlBytes, "ctrl area");
-static_assert(kCtlTail >= kCtlPair + kMaxPairs && (kCtlTail + kTailWG + 2 * kTailPairs + 2) * 4 <= kCtrlBytes, "tail stamps");
 // per-pair record (fp64) written by the last workgroup of each pair
 constexpr int P_S = 0;        // 28: JtJ upper (21), JtR (6), #invalid
 constexpr int P_CMN = 28;     // 7: JtR / count corrections of the blocks at the pair's min sigma_r ch0
@@ -472,7 +375,6 @@ struct IterParams {
   int fin_on;      // 0: records only (timing hook); 1: last workgroup finalizes
   int reverse;     // marching path: walk every band in the opposite direction (DPFT_ITER_REVERSE)
   int skew;        // marching path: band-size skew, 64ths (see ic_reduce_kernel)
-  int grid_waste;  // marching path: idle waves (64ths of a pair's) the band grid may leave
   FinParams fin;
 };
 
@@ -500,29 +402,6 @@ __device__ __forceinline__ void setup_pixel(const IterParams& p, int b, int x, i
   if (p.mask0) inv = inv || (p.mask0[(size_t)b * HW + y * W + x] == 0);
   if (p.mask1) inv = inv || !(bil_u8(p.mask1 + (size_t)b * HW, px.tp) > 0.0f);
   px.invalid = inv;
-}
-
-// Unit-normalised 3x3 Sobel of an LDS tile around (row r, col c)
-// (algorithms.py:1852-1863: cross-correlation with [-1 0 1; -2 0 2; -1 0 1]).
-__device__ __forceinline__ void sobel_lds(const float* __restrict__ L, int r, int c, float& gx, float& gy,
-                                          float& ctr) {
-  const float* a = L + (r - 1) * kLdsW + c;
-  const float* m = L + r * kLdsW + c;
-  const float* z = L + (r + 1) * kLdsW + c;
-  const float v00 = a[-1], v01 = a[0], v02 = a[1];
-  const float v10 = m[-1], v11 = m[0], v12 = m[1];
-  const float v20 = z[-1], v21 = z[0], v22 = z[1];
-  const float x = (v02 - v00) + 2.0f * (v12 - v10) + (v22 - v20);
-  const float y = (v20 + 2.0f * v21 + v22) - (v00 + 2.0f * v01 + v02);
-  const float inv = rsqrtf(x * x + y * y + 1e-8f);
-  gx = x * inv;
-  gy = y * inv;
-  ctr = v11;
-}
-
-// Same, on a 3-row stencil window (rows 0..2, centre row 1).
-__device__ __forceinline__ void sobel_lds_w(const float* __restrict__ L, int c, float& gx, float& gy, float& ctr) {
-  sobel_lds(L, 1, c, gx, gy, ctr);
 }
 
 // Warp Jacobian at the origin, xi = [rot, trs] (algorithms.py:1908-1917).
@@ -743,13 +622,16 @@ __device__ __forceinline__ IcpTerm icp_pixel(float xr, float yr, float d0, const
 // Frame-1 normal map of one level (algorithms.py:2148-2172): vertex map
 // (geometry.py:1129-1136), unnormalised replicate-padded Sobel, cross product,
 // / (|n| + 1e-8), zero where depth equals the batch-global min or max.
+// `dext`: order-encoded (min, max) word pairs, one per independent batch of `group` pairs
+// (DPFT_GROUP; group = B: the call is one batch, the reference's batch-global extrema).
 __global__ __launch_bounds__(kThreads) void icp_normals_kernel(const float* __restrict__ depth, const float* __restrict__ K,
                                                                int B, int H, int W, const uint32_t* __restrict__ dext,
-                                                               float* __restrict__ nrm) {
+                                                               int group, float* __restrict__ nrm) {
   const int HW = H * W;
   const long i = (long)blockIdx.x * kThreads + threadIdx.x;
   if (i >= (long)B * HW) return;
   const int b = (int)(i / HW), pix = (int)(i - (long)b * HW), y = pix / W, x = pix - y * W;
+  dext += 2 * (b / group);
   const float fx = K[4 * b + 0], fy = K[4 * b + 1], cx = K[4 * b + 2], cy = K[4 * b + 3];
   const float* db = depth + (size_t)b * HW;
   float V[3][3][3];  // [dy][dx][xyz]
@@ -810,13 +692,7 @@ __device__ void global_extrema(const float* rec, int nblocks, int imn, int imx, 
 // to ~2^-22, each step doubles the bits) -- a few dependent FMAs instead of the
 // correctly rounded sqrt and divide sequences on the finalize's serial path.  x = 0 and
 // x < 0 (a non-SPD pivot) give inf / NaN like 1 / sqrt(x).
-#ifndef DPFT_FIN_RSQ
-#define DPFT_FIN_RSQ 1
-#endif
 __device__ __forceinline__ double rsqrt_d(double x) {
-#if !DPFT_FIN_RSQ
-  return 1.0 / sqrt(x);
-#endif
   double r = __builtin_amdgcn_rsq(x);
   if (!(x > 0.0) || isinf(x)) return r;
 #pragma unroll
@@ -835,9 +711,6 @@ __device__ __forceinline__ double rsqrt_d(double x) {
 // epsilon there and lev_mar_H's damping here.
 __device__ void solve_and_update(const double* jtj_u, const double* jtr, float* Rp, float* tp,
                                  const double* diag_add = nullptr) {
-#if DPFT_ABL_SOLVE == 1  // profiling ablation: no solve / update
-  return;
-#endif
   double A[6][6];
   int k = 0;
 #pragma unroll
@@ -889,14 +762,7 @@ __device__ void solve_and_update(const double* jtj_u, const double* jtr, float* 
   const double k0 = w0 * ith, k1 = w1 * ith, k2 = w2 * ith;
   const double Kx[9] = {0.0, -k2, k1, k2, 0.0, -k0, -k1, k0, 0.0};
   double sn, cs;
-#if DPFT_ABL_SOLVE == 2  // profiling ablation: fp32 trig
-  float snf, csf;
-  sincosf((float)th, &snf, &csf);
-  sn = snf;
-  cs = csf;
-#else
   sincos(th, &sn, &cs);
-#endif
   const double cs1 = 1.0 - cs;
   double dR[9];
 #pragma unroll
@@ -999,11 +865,8 @@ __device__ void finalize_batch_from(const FinParams& q, Get get) {
 }
 // (Loading each pair record in one burst of 16-byte sc1 loads before the extrema are
 // known measured 6 us SLOWER per finalize than these field loads: not adopted.)
-#ifndef DPFT_FIN_BURST8
-#define DPFT_FIN_BURST8 1
-#endif
 __device__ void finalize_batch(const FinParams& q) {
-  if (!DPFT_FIN_BURST8 || q.B > kThreads) {
+  if (q.B > kThreads) {
     finalize_batch_from(q, [&](int b, int i) { return ld_ag(q.prec + (size_t)b * kPRec + i); });
     return;
   }
@@ -1114,14 +977,6 @@ __device__ void pair_reduce2(const FinParams& q, int b, float* sc) {
       }
     }
   }
-#if DPFT_TAIL_PROF
-  auto stamp = [&](int i) {
-    __builtin_amdgcn_s_waitcnt(0);
-    if (b == 0 && tid == 0) st_ag(q.pair_cnt + kCtlTail - kCtlPair + kTailWG + 2 * kTailPairs + 2 + i,
-                                  (uint32_t)wall_clock64());
-  };
-  stamp(0);
-#endif
   // pair extrema of sigma_r first (which records' corrections count)
   float ex[4] = {f[R_MN_ALL], f[R_MN0], f[R_MX_ALL], f[R_MX0]};
   if (tru) {
@@ -1137,9 +992,6 @@ __device__ void pair_reduce2(const FinParams& q, int b, float* sc) {
     ex[3] = fmaxf(fmaxf(scf[3], scf[7]), fmaxf(scf[11], scf[15]));
     __syncthreads();  // scf is reused below
   }
-#if DPFT_TAIL_PROF
-  stamp(1);
-#endif
   // fields in the pair-record order: 28 sums, then the 7 + 7 corrections (masked)
   const bool use_mn = f[R_MN0] == ex[1], use_mx = f[R_MX0] == ex[3];
   auto field = [&](int i) -> float {
@@ -1159,9 +1011,6 @@ __device__ void pair_reduce2(const FinParams& q, int b, float* sc) {
     v += __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), 0x4E, 0xf, 0xf, true));  // quad_perm 2,3,0,1
     if (i < nf && (tid & 3) == 0) L[i * 65 + (tid >> 2)] = v;
   }
-#if DPFT_TAIL_PROF
-  stamp(2);
-#endif
   __syncthreads();
   double* pr = q.prec + (size_t)b * kPRec;
   if (tid < nf) {
@@ -1219,17 +1068,15 @@ __device__ void finalize_loss(const FinParams& q) {
 //       2 = IC without uncertainty (TrustRegionBase, algorithms.py:23-139: sigma = 1,
 //           J = Jf_x Jx + Jf_y Jy (1867-1882), occluded residual 1e-3 (1955)).
 template <int CT, bool CS1, bool TRU, int MODE, bool C4>
-__global__ __launch_bounds__(kThreads, DPFT_MIN_WAVES) void ic_reduce_kernel(IterParams p) {
+__global__ __launch_bounds__(kThreads, 1) void ic_reduce_kernel(IterParams p) {
   constexpr bool ICP = MODE == 1, NOSIG = MODE == 2;
-  // (DPFT_TAIL_PROF, profiling build: finish timeline in ctrl words 16..28 and 64.., stamped only
-  // after the pass -- a stamp at the start costs the main loop registers; tools/kbench.py --tail)
   static_assert(!C4 || CS1, "the channel-quad layout needs one sigma plane");
-  constexpr int R = C4 ? ((kMarch && CT > 0) ? 1 : kRPL4) : (CS1 ? kRPL : 1);  // rows per lane
+  constexpr int R = C4 ? ((CT > 0) ? 1 : kRPL4) : (CS1 ? kRPL : 1);  // rows per lane
   constexpr float kFill = NOSIG ? 1e-3f : 1e-6f;  // weighted residual of invalid pixels
   const int C = CT > 0 ? CT : p.C;
   __shared__ float lds_ext[TRU ? 2 * 7 : 1][kThreads];  // extremum corrections (6 + count), min then max
   __shared__ float red[4][kRec];
-  constexpr bool kWin = C4 && kMarch && CT > 0;
+  constexpr bool kWin = C4 && CT > 0;  // channel-quad marching window (C = 16, 32)
   __shared__ f32x4 lds_win[kWin ? 4 : 1][kWin ? 2 * (CT / 4) * 64 : 1];  // used: 2 x NQW quads per wave
   // pair_reduce2 scratch where neither the window nor the extremum buffer is there to reuse
   __shared__ float fin_sc[(kWin || TRU) ? 1 : 28 * 65];
@@ -1280,7 +1127,7 @@ __global__ __launch_bounds__(kThreads, DPFT_MIN_WAVES) void ic_reduce_kernel(Ite
   // 62-column strip, so the stencil / tap rows shared with the tile above are more
   // often still in this XCD's L2 (measured L0 fetch 1.05 GB vs 1.13 GB row-major,
   // 212 vs 217 us).  NCHW: row-major (column-major measured 12 % slower there).
-  constexpr bool kColMajor = C4 && !DPFT_ROWMAJOR;
+  constexpr bool kColMajor = C4;
   auto tile_pos = [&](int i, int& xs, int& y) {
     const int local = i - b * p.per_pair;
     int tx, ty;
@@ -1375,9 +1222,6 @@ __global__ __launch_bounds__(kThreads, DPFT_MIN_WAVES) void ic_reduce_kernel(Ite
     }
   };
 
-  // Per-pixel counts (invalid pixels, truncated-sigma extremum pixels) and the ICP term
-  // are added by ONE of the waves that share a pixel's channels (channel-split march).
-  float cnt_w = 1.0f;
   // the seven per-pixel channel sums -> JtJ / JtR / invalid count / extremum corrections
   struct Sums {
     float Saa[R], Sab[R], Sbb[R], Sa[R], Sb[R], Sar[R], Sbr[R];
@@ -1414,8 +1258,8 @@ __global__ __launch_bounds__(kThreads, DPFT_MIN_WAVES) void ic_reduce_kernel(Ite
       }
 #pragma unroll
       for (int i = 0; i < 6; ++i) acc[21 + i] -= cA * Jx[i] + cB * Jy[i];
-      ninv += invalid ? cnt_w : 0.0f;
-      if (ICP && cnt_w != 0.0f) {  // JtWJ += (wJ)^T (wJ), JtR += (wJ)^T (w r)  (algorithms.py:668-689)
+      ninv += invalid ? 1.0f : 0.0f;
+      if (ICP) {  // JtWJ += (wJ)^T (wJ), JtR += (wJ)^T (w r)  (algorithms.py:668-689)
         const int yr = F.y0 + r;
         const float d0v = p.depth0[(size_t)b * HW + yr * W + F.xc];
         const IcpTerm ic = icp_pixel(F.wp[r].xr, F.wp[r].yr, d0v, Rm, tv, fx, fy, cx, cy, H, W,
@@ -1442,7 +1286,7 @@ __global__ __launch_bounds__(kThreads, DPFT_MIN_WAVES) void ic_reduce_kernel(Ite
           const float dB = invalid ? 0.0f : (1e-6f * Sb - Sbr);
 #pragma unroll
           for (int i = 0; i < 6; ++i) corr[i] = -(dA * Jx[i] + dB * Jy[i]);
-          corr[6] = invalid ? 0.0f : cnt_w;
+          corr[6] = invalid ? 0.0f : 1.0f;
           if (le) {
             const bool reset = sr0 < mn0;
             mn0 = sr0;
@@ -1460,7 +1304,7 @@ __global__ __launch_bounds__(kThreads, DPFT_MIN_WAVES) void ic_reduce_kernel(Ite
     }
   };
 
-  if constexpr (C4 && kMarch && CT > 0) {
+  if constexpr (kWin) {
     // ---- channel-quad layout, row-marching register window.  Each WAVE owns a
     // contiguous run of (column strip, row) units of its pair, strip-major, and walks
     // it row by row keeping the f0 rows y - dir and y of every quad (and of sigma0) in
@@ -1473,15 +1317,8 @@ __global__ __launch_bounds__(kThreads, DPFT_MIN_WAVES) void ic_reduce_kernel(Ite
     constexpr int NQ = CT / 4;
     static_assert(CT % 4 == 0, "channel quads");
     const int U = p.tiles_x * H;
-    // kMarchCSplit waves share a band, each with NQW of the NQ channel quads: the JtJ /
-    // JtR terms are linear in a pixel's channel sums, so each wave accumulates its own
-    // share with no exchange; a band row takes 1/kMarchCSplit of the time, so the f1 tap
-    // row a row shares with the next is re-requested before L2 has cycled.
-    constexpr int CSP = (NQ / kMarchCSplit >= 2) ? kMarchCSplit : (NQ >= 4 ? NQ / 2 : 1), NQW = NQ / CSP;
-    static_assert(NQ % CSP == 0 && 4 % CSP == 0, "channel split");
-    const int jw = jb * 4 + wave, band = jw / CSP, sub = jw - band * CSP, nw = p.nbpp * 4 / CSP;
-    const int qbase = sub * NQW;
-    cnt_w = sub == 0 ? 1.0f : 0.0f;
+    constexpr int NQW = NQ;                            // every quad of a pixel in one wave
+    const int band = jb * 4 + wave, nw = p.nbpp * 4;  // this wave's band, the pair's waves
     // Band sizes: the first half of a pair's waves belongs to the workgroups dispatched
     // first, which the oldest-first issue arbitration favours over the second
     // workgroup on the same CU; equal bands leave the second half running alone
@@ -1500,12 +1337,12 @@ __global__ __launch_bounds__(kThreads, DPFT_MIN_WAVES) void ic_reduce_kernel(Ite
     // L2 hit for the second) instead of tens of microseconds apart.  Up to nw / 16 waves
     // may be left without a band (nw - K S); otherwise the strip-major split below.
     const int S_ = p.tiles_x, K_ = nw / S_;
-    const bool grid = kMarchGrid && K_ >= 2 && (nw - K_ * S_) * 64 <= nw * p.grid_waste;
+    const bool grid = K_ >= 2 && (nw - K_ * S_) * 64 <= nw * kGridWaste;
     int ubeg, uend, vband;
     // hybrid split: wave s < S owns rows [0, T_s) of strip s, T_s its weighted share of
     // the pair's units (Tf for the first half of the waves, Tu for the second); the
     // nw - S pool waves split the bottom rows [T_s, H) of all strips, strip-major
-    const bool hyb = kMarchHybrid && !grid && nw > S_ && nw < 2 * S_;
+    const bool hyb = !grid && nw > S_ && nw < 2 * S_;
     const int hh = nw >> 1, hsk = nw >= 2 ? p.skew : 0;
     const int hwt = (64 + hsk) * hh + (64 - hsk) * (nw - hh);
     const int hTf = min(H, (U * (64 + hsk)) / hwt), hTu = min(H, (U * (64 - hsk)) / hwt);
@@ -1540,7 +1377,7 @@ __global__ __launch_bounds__(kThreads, DPFT_MIN_WAVES) void ic_reduce_kernel(Ite
     const int nrows = uend - ubeg;
     // odd iterations reverse every band: they start on the rows the previous iteration
     // read last, which are still in the Infinity Cache
-    const bool up = ((vband & 1) != 0) != (kMarchReverse && p.reverse != 0);
+    const bool up = ((vband & 1) != 0) != (p.reverse != 0);
     const int dir = up ? -1 : 1;
     const float dirf = up ? -1.0f : 1.0f;
     // unit k of the wave's run -> (lane column xs, row y); strt: a strip begins at this
@@ -1579,14 +1416,14 @@ __global__ __launch_bounds__(kThreads, DPFT_MIN_WAVES) void ic_reduce_kernel(Ite
       f32x4 f;      // f0 row y + dir
       f32x4 t[4];   // f1 taps (see gather4 / QuadLoadsR); tap cache: trailing pair, leading pair
     };
-    // Tap cache (kTapCache): in marching order, the f1 tap row a pixel row shares with
+    // Tap cache: in marching order, the f1 tap row a pixel row shares with
     // the next one is its LEADING row (lower row marching down, upper row marching up)
     // and the next row's TRAILING row.  Each lane keeps its leading pair of every quad
     // (pair base `tc_ob`) and the next row reloads its trailing pair only where the
     // pair base differs: a hit returns exactly the bytes a load of that base would
     // (f1 is read-only), so the cache changes no result, only the f1 re-fetch that
     // otherwise misses the XCD's L2 one row-step later.
-    f32x4 tc[kTapCache ? NQW : 1][2];
+    f32x4 tc[NQW][2];
     int tc_ob = -1;
 
     // d of the next step's (up to) two rows, prefetched one step ahead
@@ -1600,156 +1437,85 @@ __global__ __launch_bounds__(kThreads, DPFT_MIN_WAVES) void ic_reduce_kernel(Ite
       }
     };
     if (nrows > 0) load_d2(0, dnx);
-    // One marching step of NS rows (2, or 1 at an odd end / a strip change).  Channel work
-    // goes in units (quad q, row r), rows innermost, so the f1 tap row a pixel of row y
-    // shares with the pixel below it is requested twice back to back (an L1/L2 hit)
-    // instead of one row-step later (after L2 has dropped it: 1.55x f1 traffic).
-    // Window slots: slot 0 = row y - dir, slot 1 = row y; unit (q, 0) reads both and
-    // leaves row y + dir in slot 0, unit (q, 1) reads slot 1 / slot 0 and leaves y + 2 dir
-    // in slot 1, which is the window of the next step.
-    auto stepn = [&](auto NSC, int k) {
-      constexpr int NS = decltype(NSC)::value;
-      constexpr int NU = NQW * NS;
-      int xs, yr[NS];
+    // One marching step: row y of the wave's strip.  Window slots (LDS): slot 0 = row
+    // y - dir, slot 1 = row y; quad q reads both and leaves (y, y + dir) for the next step.
+    // The quad loop is straight-line with static quad indices (the tap cache lives in
+    // registers), kRingQ quads in flight.
+    auto step = [&](int k) {
+      int xs, y;
       bool strt0;
-      unit_pos_st(k, xs, yr[0], strt0);
-      if constexpr (NS == 2) {
-        int xs1;
-        unit_pos(k + 1, xs1, yr[1]);
-      }
-      const float dcur[2] = {dnx[0], dnx[1]};
-      if (k + NS < nrows) load_d2(k + NS, dnx);
+      unit_pos_st(k, xs, y, strt0);
+      const float dcur = dnx[0];
+      if (k + 1 < nrows) load_d2(k + 1, dnx);
       const int colq = min(max(xs, 0), W - 1) * 16;
       if (k == 0 || strt0) {  // prime the window: rows y - dir (replicate-clamped) and y
-        const int yp = min(max(yr[0] - dir, 0), H - 1);
+        const int yp = min(max(y - dir, 0), H - 1);
 #pragma unroll
         for (int q = 0; q < NQW; ++q) {
-          const int po = (qbase + q) * 4 * (int)planeB;
+          const int po = q * 4 * (int)planeB;
           win[q * 64 + lane] = llvm_buf_load_f32x4(rf0, colq, po + yp * W * 16, kF0Aux);
-          win[(NQW + q) * 64 + lane] = llvm_buf_load_f32x4(rf0, colq, po + yr[0] * W * 16, kF0Aux);
+          win[(NQW + q) * 64 + lane] = llvm_buf_load_f32x4(rf0, colq, po + y * W * 16, kF0Aux);
         }
         if (CS1 && !NOSIG) {
           sprev = bld(rs0, colq >> 2, yp * W * 4);
-          scur = bld(rs0, colq >> 2, yr[0] * W * 4);
+          scur = bld(rs0, colq >> 2, y * W * 4);
         }
       }
-      int yn[NS];
-      Frame F[NS];
-      float snew[NS];
-#pragma unroll
-      for (int r = 0; r < NS; ++r) {
-        yn[r] = min(max(yr[r] + dir, 0), H - 1);
-        const float dv[1] = {dcur[r]};
-        make_frame_xy(xs, yr[r], dv, F[r], false);
-        snew[r] = (CS1 && !NOSIG) ? bld(rs0, colq >> 2, yn[r] * W * 4) : 0.f;
+      const int yn = min(max(y + dir, 0), H - 1);
+      Frame F;
+      {
+        const float dv[1] = {dcur};
+        make_frame_xy(xs, y, dv, F, false);
       }
-      // straight-line quad loop (one row per step): a ring of kRingQ quads, kRingQ - 1 ahead
-      constexpr bool kLine = DPFT_UNROLL_Q && NS == 1;
-      constexpr int RM = kLine ? (kRingQ < NQW ? kRingQ : NQW) : kRingM;
+      const float snew = (CS1 && !NOSIG) ? bld(rs0, colq >> 2, yn * W * 4) : 0.f;
+      constexpr int RM = kRingQ < NQW ? kRingQ : NQW;
+      static_assert(RM >= 2 && RM <= NQW, "ring depth");
       QuadM L[RM];
-      // tap cache: trailing / leading pair bases and weights of this row (NS == 1)
-      const int obT = up ? F[0].tp[0].ob1 : F[0].tp[0].ob0, obL = up ? F[0].tp[0].ob0 : F[0].tp[0].ob1;
-      const bool tc_hit = kTapCache && NS == 1 && obT == tc_ob;
-      PairWeights wq = F[0].pw[0];  // channel-unit weights of slots t[0..3]
-      if constexpr (kTapCache && NS == 1) {
-        tc_ob = obL;
-        if (up) {  // slots 0/1 hold the trailing pair: the lower row when marching up
-          wq.w0 = F[0].pw[0].w2;
-          wq.w1 = F[0].pw[0].w3;
-          wq.w2 = F[0].pw[0].w0;
-          wq.w3 = F[0].pw[0].w1;
-        }
+      // tap cache: trailing / leading pair bases and weights of this row
+      const int obT = up ? F.tp[0].ob1 : F.tp[0].ob0, obL = up ? F.tp[0].ob0 : F.tp[0].ob1;
+      const bool tc_hit = obT == tc_ob;
+      PairWeights wq = F.pw[0];  // channel-unit weights of slots t[0..3]
+      tc_ob = obL;
+      if (up) {  // slots 0/1 hold the trailing pair: the lower row when marching up
+        wq.w0 = F.pw[0].w2;
+        wq.w1 = F.pw[0].w3;
+        wq.w2 = F.pw[0].w0;
+        wq.w3 = F.pw[0].w1;
       }
-      auto issue = [&](QuadM& Qm, int q, auto RC) {
-        constexpr int r = decltype(RC)::value;
-#if DPFT_ABL == 1  // profiling ablation: no channel loop (frame + epilogue only)
-        return;
-#endif
-        const int po = (qbase + q) * 4 * (int)planeB;
-        Qm.f = llvm_buf_load_f32x4(rf0, colq, po + yn[r] * W * 16, kF0Aux);
-#if DPFT_ABL == 3  // profiling ablation: no f1 gathers
-        Qm.t[0] = Qm.t[1] = Qm.t[2] = Qm.t[3] = Qm.f;
-#else
-        if constexpr (kTapCache && NS == 1) {
-          // branch-free: a hit lane re-requests its leading pair (an L1 hit next to the
-          // leading loads below) and selects the cached bytes; a divergent branch around
-          // the loads would make the waitcnt bookkeeping wait on the next quad's loads
-          // (the select happens at use, in unitc: here it would wait on the load at once)
-          const int offT = (tc_hit ? obL : obT) * 16;
-          Qm.t[0] = bld4(rf1, offT, po);
-          Qm.t[1] = bld4(rf1, offT + 16, po);
-          Qm.t[2] = bld4(rf1, obL * 16, po);
-          Qm.t[3] = bld4(rf1, obL * 16 + 16, po);
-        } else {
-          Qm.t[0] = bld4(rf1, F[r].tp[0].ob0 * 16, po);
-          Qm.t[1] = bld4(rf1, F[r].tp[0].ob0 * 16 + 16, po);
-          Qm.t[2] = bld4(rf1, F[r].tp[0].ob1 * 16, po);
-          Qm.t[3] = bld4(rf1, F[r].tp[0].ob1 * 16 + 16, po);
-        }
-#endif
+      auto issue = [&](QuadM& Qm, int q) {
+        const int po = q * 4 * (int)planeB;
+        Qm.f = llvm_buf_load_f32x4(rf0, colq, po + yn * W * 16, kF0Aux);
+        // branch-free: a hit lane re-requests its leading pair (an L1 hit next to the
+        // leading loads below) and selects the cached bytes; a divergent branch around
+        // the loads would make the waitcnt bookkeeping wait on the next quad's loads
+        // (the select happens at use, in unitc: here it would wait on the load at once)
+        const int offT = (tc_hit ? obL : obT) * 16;
+        Qm.t[0] = bld4(rf1, offT, po);
+        Qm.t[1] = bld4(rf1, offT + 16, po);
+        Qm.t[2] = bld4(rf1, obL * 16, po);
+        Qm.t[3] = bld4(rf1, obL * 16 + 16, po);
       };
-      static_assert(kLine || (kRingM == 2 && NQW % 2 == 0), "two units in flight, whole (quad, row) groups per round");
-      static_assert(!kLine || (RM >= 2 && RM <= NQW), "ring depth");
 #pragma unroll
-      for (int i = 0; i < (kLine ? RM - 1 : 1); ++i) issue(L[i], i, WaveIdx<0>{});
+      for (int i = 0; i < RM - 1; ++i) issue(L[i], i);
       if (CS1 && !NOSIG) {
-        // sigma0 rows top / centre / bottom of each row (marching direction folded in)
-        const float s1n = snew[0], s2n = snew[NS - 1];
-        F[0].s0r[0] = up ? s1n : sprev;
-        F[0].s0r[1] = scur;
-        F[0].s0r[2] = up ? sprev : s1n;
-        if constexpr (NS == 2) {
-          F[1].s0r[0] = up ? s2n : scur;
-          F[1].s0r[1] = s1n;
-          F[1].s0r[2] = up ? scur : s2n;
-          sprev = s1n;
-          scur = s2n;
-        } else {
-          sprev = scur;
-          scur = s1n;
-        }
+        // sigma0 rows top / centre / bottom (marching direction folded in)
+        F.s0r[0] = up ? snew : sprev;
+        F.s0r[1] = scur;
+        F.s0r[2] = up ? sprev : snew;
+        sprev = scur;
+        scur = snew;
       }
-      // The occlusion / sigma terms only enter the epilogue (the channel sums are
-      // weight-free), so on the straight-line path they are resolved after the channel
-      // loop: the frame's depth / sigma1 gathers land behind it instead of stalling here.
-      PixelTerms T[NS];
-      if constexpr (!(kLine && kLateTerms)) {
+      PixelTerms T;
+      pixel_terms(F, T);
+      f32x2 Q[9];
 #pragma unroll
-        for (int r = 0; r < NS; ++r) pixel_terms(F[r], T[r]);
-      }
-      f32x2 Q[NS][9];
-#pragma unroll
-      for (int r = 0; r < NS; ++r)
-#pragma unroll
-        for (int i = 0; i < 9; ++i) Q[r][i] = f32x2{0.f, 0.f};
-      auto unitc = [&](int q, const QuadM& cur, auto RC) {
-        constexpr int r = decltype(RC)::value;
-#if DPFT_ABL == 1
-        return;
-#endif
+      for (int i = 0; i < 9; ++i) Q[i] = f32x2{0.f, 0.f};
+      auto unitc = [&](int q, const QuadM& cur) {
         f32x4* s0p = win + q * 64 + lane;          // slot 0
         f32x4* s1p = win + (NQW + q) * 64 + lane;  // slot 1
-        f32x4 wtop, wmid;  // rows above / at the pixel in marching order
-        if constexpr (r == 0) {
-          wtop = *s0p;
-          wmid = *s1p;
-        } else {
-          wtop = *s1p;
-          wmid = *s0p;
-        }
-#if DPFT_ABL == 2  // profiling ablation: loads only
-        {
-          const f32x4 z = wtop + wmid + cur.f + cur.t[0] + cur.t[1] + cur.t[2] + cur.t[3];
-          Q[r][0] += f32x2{z.x, z.y};
-          Q[r][1] += f32x2{z.z, z.w};
-        }
-#else
-        const PairWeights& w = (kTapCache && NS == 1) ? wq : F[r].pw[0];
-        f32x4 tt0 = cur.t[0], tt1 = cur.t[1];  // trailing pair (cached bytes on a hit)
-        if constexpr (kTapCache && NS == 1) {
-          tt0 = tc_hit ? tc[q][0] : tt0;
-          tt1 = tc_hit ? tc[q][1] : tt1;
-        }
+        const f32x4 wtop = *s0p, wmid = *s1p;      // rows above / at the pixel in marching order
+        const f32x4 tt0 = tc_hit ? tc[q][0] : cur.t[0];  // trailing pair (cached bytes on a hit)
+        const f32x4 tt1 = tc_hit ? tc[q][1] : cur.t[1];
 #pragma unroll
         for (int h = 0; h < 2; ++h) {  // channels 4q + 2h, 4q + 2h + 1
           auto half = [&](const f32x4& v) { return h ? f32x2{v.z, v.w} : f32x2{v.x, v.y}; };
@@ -1772,101 +1538,51 @@ __global__ __launch_bounds__(kThreads, DPFT_MIN_WAVES) void ic_reduce_kernel(Ite
           const f32x2 n2 = x * x + (yv * yv + 1e-8f);
           const f32x2 inv = f32x2{__builtin_amdgcn_rsqf(n2.x), __builtin_amdgcn_rsqf(n2.y)};
           const f32x2 gx = x * inv, gy = yv * inv;
-          const f32x2 res = ((half(tt0) * w.w0 - fm) + half(tt1) * w.w1) + half(cur.t[2]) * w.w2 +
-                            half(cur.t[3]) * w.w3;
-          Q[r][0] += gx * gx;
-          Q[r][1] += gx * gy;
-          Q[r][2] += gy * gy;
-          Q[r][3] += gx * res;
-          Q[r][4] += gy * res;
-          Q[r][5] += res * res;
-          Q[r][6] += gx;
-          Q[r][7] += gy;
-          Q[r][8] += res;
+          const f32x2 res = ((half(tt0) * wq.w0 - fm) + half(tt1) * wq.w1) + half(cur.t[2]) * wq.w2 +
+                            half(cur.t[3]) * wq.w3;
+          Q[0] += gx * gx;
+          Q[1] += gx * gy;
+          Q[2] += gy * gy;
+          Q[3] += gx * res;
+          Q[4] += gy * res;
+          Q[5] += res * res;
+          Q[6] += gx;
+          Q[7] += gy;
+          Q[8] += res;
         }
-#endif
-        if constexpr (kTapCache && NS == 1) {  // the leading pair is the next row's trailing pair
-          tc[q][0] = cur.t[2];
-          tc[q][1] = cur.t[3];
-        }
-#if DPFT_UNROLL_Q
+        tc[q][0] = cur.t[2];  // the leading pair is the next row's trailing pair
+        tc[q][1] = cur.t[3];
         // straight-line code: the accumulators are pure arithmetic, which the DAG scheduler
         // would otherwise sink below every later load (all quads' loads first: 400 VGPRs)
-        asm volatile("" : "+v"(Q[r][0]), "+v"(Q[r][1]), "+v"(Q[r][2]), "+v"(Q[r][3]), "+v"(Q[r][4]),
-                     "+v"(Q[r][5]), "+v"(Q[r][6]), "+v"(Q[r][7]), "+v"(Q[r][8])::"memory");
-#endif
-        if constexpr (NS == 1) {  // window (y, y + dir)
-          *s0p = wmid;
-          *s1p = cur.f;
-        } else if constexpr (r == 0) {
-          *s0p = cur.f;
-        } else {
-          *s1p = cur.f;
-        }
+        asm volatile("" : "+v"(Q[0]), "+v"(Q[1]), "+v"(Q[2]), "+v"(Q[3]), "+v"(Q[4]), "+v"(Q[5]), "+v"(Q[6]),
+                     "+v"(Q[7]), "+v"(Q[8])::"memory");
+        *s0p = wmid;  // window (y, y + dir)
+        *s1p = cur.f;
       };
-      if constexpr (kLine) {
-        // static quad indices (the tap cache lives in registers); each unit's accumulators
-        // are pinned at its end (unitc), so the rounds keep this order
+      // each unit's accumulators are pinned at its end (unitc), so the rounds keep this order
 #pragma unroll
-        for (int qq = 0; qq < NQW; ++qq) {
-          if (qq + RM - 1 < NQW) issue(L[(qq + RM - 1) % RM], qq + RM - 1, WaveIdx<0>{});
-          unitc(qq, L[qq % RM], WaveIdx<0>{});
-        }
-      } else {
-        // every ring round but the last refills unconditionally: each load set keeps its registers
-        constexpr int r1 = 1 % NS;  // row of the odd units
-#pragma unroll 1
-        for (int u0 = 0; u0 < NU - 2; u0 += 2) {
-          issue(L[1], (u0 + 1) / NS, WaveIdx<r1>{});
-          unitc(u0 / NS, L[0], WaveIdx<0>{});
-          issue(L[0], (u0 + 2) / NS, WaveIdx<0>{});
-          unitc((u0 + 1) / NS, L[1], WaveIdx<r1>{});
-        }
-        issue(L[1], (NU - 1) / NS, WaveIdx<r1>{});
-        unitc((NU - 2) / NS, L[0], WaveIdx<0>{});
-        unitc((NU - 1) / NS, L[1], WaveIdx<r1>{});
+      for (int qq = 0; qq < NQW; ++qq) {
+        if (qq + RM - 1 < NQW) issue(L[(qq + RM - 1) % RM], qq + RM - 1);
+        unitc(qq, L[qq % RM]);
       }
-      if constexpr (kLine && kLateTerms) {
+      Sums S;
+      float q[9];
 #pragma unroll
-        for (int r = 0; r < NS; ++r) pixel_terms(F[r], T[r]);
-      }
-#pragma unroll
-      for (int r = 0; r < NS; ++r) {
-        Sums S;
-        float q[9];
-#pragma unroll
-        for (int i = 0; i < 9; ++i) q[i] = Q[r][i].x + Q[r][i].y;
-        q[1] *= dirf;  // gy was accumulated in marching order
-        q[4] *= dirf;
-        q[7] *= dirf;
-        const float A = T[r].inv_s[0], bx = T[r].kk[0] * T[r].hx[0], by = T[r].kk[0] * T[r].hy[0], A2 = A * A;
-        S.Saa[0] = A2 * q[0] + 2.0f * A * bx * q[3] + bx * bx * q[5];
-        S.Sab[0] = A2 * q[1] + A * by * q[3] + A * bx * q[4] + bx * by * q[5];
-        S.Sbb[0] = A2 * q[2] + 2.0f * A * by * q[4] + by * by * q[5];
-        S.Sa[0] = A * q[6] + bx * q[8];
-        S.Sb[0] = A * q[7] + by * q[8];
-        S.Sar[0] = A2 * q[3] + A * bx * q[5];
-        S.Sbr[0] = A2 * q[4] + A * by * q[5];
-        finish_pixels(F[r], T[r], S);
-      }
+      for (int i = 0; i < 9; ++i) q[i] = Q[i].x + Q[i].y;
+      q[1] *= dirf;  // gy was accumulated in marching order
+      q[4] *= dirf;
+      q[7] *= dirf;
+      const float A = T.inv_s[0], bx = T.kk[0] * T.hx[0], by = T.kk[0] * T.hy[0], A2 = A * A;
+      S.Saa[0] = A2 * q[0] + 2.0f * A * bx * q[3] + bx * bx * q[5];
+      S.Sab[0] = A2 * q[1] + A * by * q[3] + A * bx * q[4] + bx * by * q[5];
+      S.Sbb[0] = A2 * q[2] + 2.0f * A * by * q[4] + by * by * q[5];
+      S.Sa[0] = A * q[6] + bx * q[8];
+      S.Sb[0] = A * q[7] + by * q[8];
+      S.Sar[0] = A2 * q[3] + A * bx * q[5];
+      S.Sbr[0] = A2 * q[4] + A * by * q[5];
+      finish_pixels(F, T, S);
     };
-    for (int k = 0; k < nrows;) {
-      // two rows per step unless only one is left or the second starts a new strip
-      bool two = kMarchRows == 2 && k + 1 < nrows;
-      if (two) {
-        int xs1, y1;
-        bool strt1;
-        unit_pos_st(k + 1, xs1, y1, strt1);
-        two = !strt1;
-      }
-      if (two) {
-        stepn(WaveIdx<2>{}, k);
-        k += 2;
-      } else {
-        stepn(WaveIdx<1>{}, k);
-        k += 1;
-      }
-    }
+    for (int k = 0; k < nrows; ++k) step(k);
   } else if constexpr (C4) {
     // ---- channel-quad layout: the per-pixel weights factor out of the channel sums
     // (alpha = 1/sigma, bx = kk hx, by = kk hy give na = alpha gx + bx r,
@@ -1915,10 +1631,6 @@ __global__ __launch_bounds__(kThreads, DPFT_MIN_WAVES) void ic_reduce_kernel(Ite
           for (int k = 0; k < 9; ++k) Q[r][k] = f32x2{0.f, 0.f};
         // two channels of row r (lane-neighbour terms by DPP per half)
         auto chan2 = [&](int r, f32x2 ft, f32x2 fm, f32x2 fb, f32x2 t0, f32x2 t1, f32x2 t2, f32x2 t3) {
-#if DPFT_ABL == 2
-          Q[r][0] += ft + fm + fb + t0 + t1 + t2 + t3;
-          return;
-#endif
           const f32x2 V = ft + 2.0f * fm + fb;
           const f32x2 D = fb - ft;
           const f32x2 x = f32x2{lane_from_right(V.x) - lane_from_left(V.x), lane_from_right(V.y) - lane_from_left(V.y)};
@@ -1940,9 +1652,6 @@ __global__ __launch_bounds__(kThreads, DPFT_MIN_WAVES) void ic_reduce_kernel(Ite
           Q[r][8] += res;
         };
         auto unit = [&](int k, QuadLoadsR<R>& cur, QuadLoadsR<R>& nxt, bool refill) {
-#if DPFT_ABL == 1
-          return;
-#endif
           if (refill && k + kRing - 1 < nch) issue4(F, nxt, k + kRing - 1);
           if (k >= nch) return;
 #pragma unroll
@@ -2147,38 +1856,16 @@ __global__ __launch_bounds__(kThreads, DPFT_MIN_WAVES) void ic_reduce_kernel(Ite
     for (int k = 0; k < 6; ++k) st_ag(out + R_CMX + k, (float)(e.c[k]));
   }
   // the last workgroup of a pair reduces its records; the one completing the batch solves
-#if DPFT_TAIL_PROF  // no atomics: a shared min / max word serialises every workgroup's finish
-  if (threadIdx.x == 0 && kb < kTailWG) st_ag(p.ctrl + kCtlTail + kb, (uint32_t)wall_clock64());
-#endif
   // the batch-last workgroup reduces every pair's records and solves (LDS scratch: the
   // marching window, else the extremum buffer -- both dead by now)
   if (p.fin_on && block_is_last(p.fin.pair_cnt + b, 1u, (uint32_t)p.nbpp)) {
-#if DPFT_TAIL_PROF
-    const uint32_t t_pl = (uint32_t)wall_clock64();
-#endif
     if constexpr (kWin)
       pair_reduce2(p.fin, b, reinterpret_cast<float*>(&lds_win[0][0]));
     else if constexpr (TRU)
       pair_reduce2(p.fin, b, &lds_ext[0][0]);
     else
       pair_reduce2(p.fin, b, fin_sc);
-#if DPFT_TAIL_PROF
-    if (threadIdx.x == 0 && b < kTailPairs) {
-      st_ag(p.ctrl + kCtlTail + kTailWG + 2 * b, t_pl);
-      st_ag(p.ctrl + kCtlTail + kTailWG + 2 * b + 1, (uint32_t)wall_clock64());
-    }
-#endif
-#if DPFT_TAIL_PROF
-    const uint32_t t19 = (uint32_t)wall_clock64();  // (before the batch-last handshake)
-#endif
-    [[maybe_unused]] const bool solved = finalize_group(p.fin, b);
-#if DPFT_TAIL_PROF
-    __syncthreads();
-    if (threadIdx.x == 0 && solved) {
-      st_ag(p.ctrl + kCtlTail + kTailWG + 2 * kTailPairs, t19);
-      st_ag(p.ctrl + kCtlTail + kTailWG + 2 * kTailPairs + 1, (uint32_t)wall_clock64());
-    }
-#endif
+    finalize_group(p.fin, b);
   }
 }
 
@@ -2322,9 +2009,6 @@ struct SplitAcc {
 
 // Stand-alone finalize (one workgroup per pair): pair records, then the batch solve.
 __global__ __launch_bounds__(kThreads) void finalize_kernel(FinParams q) {
-#if DPFT_ABL_SOLVE == 3  // profiling ablation: empty finalize launch
-  return;
-#endif
   __shared__ float sc[kFinScratch];
   pair_reduce2(q, blockIdx.x, sc);
   finalize_group(q, blockIdx.x);
@@ -2495,7 +2179,6 @@ __device__ __forceinline__ void split_pass(const IterParams& p, int b, int jb, i
 
 template <int CT, bool TRU, int MODE>
 __global__ __launch_bounds__(kThreads, 4) void ic_split_kernel(IterParams p) {  // 4 waves per SIMD: <= 128 VGPRs
-  constexpr bool NOSIG = MODE == 2;
   static_assert(MODE != 1, "combine_ICP runs on ic_reduce_kernel");
   constexpr int NQ = CT / 4, QW = NQ / 4;
   static_assert(CT % 16 == 0 && QW >= 1, "4 waves x whole channel quads");
@@ -2507,10 +2190,6 @@ __global__ __launch_bounds__(kThreads, 4) void ic_split_kernel(IterParams p) {  
   const int b = kb / p.nbpp, jb = kb - b * p.nbpp;
   split_pass<CT, TRU, MODE>(p, b, jb, p.nbpp, qs, lds_ext, red, p.rec + (size_t)kb * kRec);
 
-  if (!kSplitSepFin && p.fin_on && block_is_last(p.fin.pair_cnt + b, 1u, (uint32_t)p.nbpp)) {
-    pair_reduce2(p.fin, b, &qs[0][0][0][0]);  // LDS scratch: the channel-sum buffers
-    finalize_group(p.fin, b);
-  }
 }
 
 // ============================================================ residual-only kernel
@@ -2935,7 +2614,6 @@ int check_desc(const DpftLevelDesc* d) {
     if (d->B % gs != 0 || d->B / gs > kMaxGroups)
       return fail(DPFT_E_INVALID, "DPFT_GROUP(%d): B=%d must be a multiple of it, at most %d batches", gs, d->B,
                   kMaxGroups);
-    if (d->flags & DPFT_COMBINE_ICP) return fail(DPFT_E_INVALID, "DPFT_GROUP: not with COMBINE_ICP");
   }
   return DPFT_OK;
 }
@@ -3034,16 +2712,6 @@ IterParams make_params(const DpftLevelDesc& d, const DpftLevelTensors& tt, const
   p.fin_on = 0;
   p.reverse = 0;
   p.skew = kMarchSkew;
-  static const int skew_env = [] {  // tuning only; read once, clamped: band weights 64 -/+ skew stay positive
-    const char* e = getenv("DPFT_DEBUG_SKEW");
-    return e ? std::min(std::max(atoi(e), 0), 63) : -1;
-  }();
-  if (skew_env >= 0) p.skew = skew_env;
-  static const int waste_env = [] {  // tuning only
-    const char* e = getenv("DPFT_DEBUG_GRID_WASTE");
-    return e ? std::min(std::max(atoi(e), 0), 63) : 4;
-  }();
-  p.grid_waste = waste_env;
   memset(&p.fin, 0, sizeof(p.fin));
   p.fin.rec = p.rec;
   p.fin.prec = reinterpret_cast<double*>(static_cast<char*>(ws) + kCtrlBytes);
@@ -3071,23 +2739,51 @@ int minmax_into(const float* src, size_t n, uint32_t* ctrl, int slot, hipStream_
   return hip_check("minmax_kernel");
 }
 
+// Extrema of `groups` consecutive batches of n floats each in one launch (minmax_levels_kernel
+// with one level, blockIdx.y = batch): batch g's (min, max) into ctrl[word + 2 g], ctrl[word + 2 g + 1].
+int minmax_batches(const float* src, size_t n, int groups, uint32_t* ctrl, int word, hipStream_t st) {
+  MMLevels a;
+  for (int l = 0; l < 4; ++l) {
+    a.s[l] = src;
+    a.n[l] = n;
+    a.slot[l] = word;
+  }
+  a.groups = groups;
+  const int grid = (int)std::max<size_t>(
+      1, std::min<size_t>(std::min<size_t>((n + kThreads * 16 - 1) / (kThreads * 16), kMMGrid),
+                          (size_t)kMaxMMBlocks / (size_t)groups));
+  hipLaunchKernelGGL(minmax_levels_kernel, dim3(grid, groups), dim3(kThreads), 0, st, a, ctrl);
+  return hip_check("minmax_levels_kernel (batches)");
+}
+
 // Pose-independent per-level pre-passes (first iteration of a level):
 // sigma0 batch extrema (truncated sigma), depth1 batch extrema + normal map (ICP).
 int launch_minmax(const DpftLevelDesc& d, const DpftLevelTensors& tt, void* ws, hipStream_t st) {
   uint32_t* ctrl = reinterpret_cast<uint32_t*>(ws);
   int rc;
   if ((d.flags & DPFT_REMOVE_TRU_SIGMA) && !(d.flags & DPFT_EXTREMA_READY)) {
-    const int gs = group_of(d);  // one pass per independent batch (DPFT_GROUP)
+    const int gs = group_of(d);  // one extremum pair per independent batch (DPFT_GROUP)
     const size_t n = (size_t)gs * d.Cs * d.H * d.W;
-    for (int g = 0; g < d.B / gs; ++g)
-      if ((rc = minmax_into(tt.s0 + g * n, n, ctrl, ext_word(d) + 2 * g, st))) return rc;
+    if (gs < d.B) {
+      if ((rc = minmax_batches(tt.s0, n, d.B / gs, ctrl, ext_word(d), st))) return rc;
+    } else if ((rc = minmax_into(tt.s0, n, ctrl, ext_word(d), st))) {
+      return rc;
+    }
   }
   if (d.flags & DPFT_COMBINE_ICP) {
+    // depth1 min / max per independent batch (algorithms.py:2168 compares against the
+    // whole batch the call holds), then frame 1's normal map
+    const int gs = group_of(d);
+    const int word = gs < d.B ? kCtlGD1 : kCtlD1Min;
+    if (gs < d.B) {  // every batch in one launch (blockIdx.y = batch)
+      if ((rc = minmax_batches(tt.depth1, (size_t)gs * d.H * d.W, d.B / gs, ctrl, word, st))) return rc;
+    } else if ((rc = minmax_into(tt.depth1, (size_t)d.B * d.H * d.W, ctrl, word, st))) {
+      return rc;
+    }
     const size_t n = (size_t)d.B * d.H * d.W;
-    if ((rc = minmax_into(tt.depth1, n, ctrl, kCtlD1Min, st))) return rc;
     float* nrm = reinterpret_cast<float*>(static_cast<char*>(ws) + nrm_offset(d));
     hipLaunchKernelGGL(icp_normals_kernel, dim3((unsigned)((n + kThreads - 1) / kThreads)), dim3(kThreads), 0, st,
-                       tt.depth1, tt.K, d.B, d.H, d.W, ctrl + kCtlD1Min, nrm);
+                       tt.depth1, tt.K, d.B, d.H, d.W, ctrl + word, gs, nrm);
     if ((rc = hip_check("icp_normals_kernel"))) return rc;
   }
   return DPFT_OK;
@@ -3110,9 +2806,7 @@ int resident_blocks(const void* kernel, int threads = kThreads) {
   if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kernel, threads, 0) != hipSuccess ||
       hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
     return 0;
-  int n = std::max(1, std::min(per_cu * cus, kMaxGrid));
-  if (const char* e = getenv("DPFT_DEBUG_GRID_CAP"))  // tuning / profiling only
-    n = std::max(1, std::min(atoi(e), kMaxGrid));
+  const int n = std::max(1, std::min(per_cu * cus, kMaxGrid));
   cache.push_back({kernel, dev, n});
   return n;
 }
@@ -3122,19 +2816,12 @@ int launch_reduce_k(IterParams p, hipStream_t st) {
   const void* k = reinterpret_cast<const void*>(&ic_reduce_kernel<CT, CS1, TRU, MODE, C4>);
   const int cap = resident_blocks(k);
   if (cap <= 0) return fail(DPFT_E_HIP, "occupancy query failed");
-  static const int rounds = [] {  // tuning only: dispatch rounds of the grid (default 1)
-    const char* e = getenv("DPFT_DEBUG_ROUNDS");
-    return e ? std::min(std::max(atoi(e), 1), 8) : 1;
-  }();
-  p.nbpp = std::max(1, std::min(cap * rounds / p.B, p.per_pair));
+  p.nbpp = std::max(1, std::min(cap / p.B, p.per_pair));  // one dispatch round
   if ((long)p.B * p.nbpp > kMaxGrid) p.nbpp = std::max(1, kMaxGrid / p.B);
   p.round_wg = cap / 8;
   p.fin.nbpp = p.nbpp;
-  // finalize in-kernel (last-workgroup handshake) or as its own one-workgroup launch
-  const bool sep = p.fin_on && (long)p.H * p.W <= kSepFinMaxPixels;
-  if (sep) p.fin_on = 0;
+  // the finalize runs in-kernel (last-workgroup handshake, fin_on)
   hipLaunchKernelGGL((ic_reduce_kernel<CT, CS1, TRU, MODE, C4>), dim3(p.B * p.nbpp), dim3(kThreads), 0, st, p);
-  if (sep) hipLaunchKernelGGL(finalize_kernel, dim3(p.B), dim3(kThreads), 0, st, p.fin);
   return DPFT_OK;
 }
 
@@ -3165,10 +2852,10 @@ int launch_split(IterParams p, hipStream_t st) {
   // Many small workgroups finish together here: the last-block handshake would
   // serialise B * nbpp atomics on B counters, so the finalize is its own launch
   // (B workgroups, the kernel boundary orders the records).
-  const bool sep = kSplitSepFin && p.fin_on;
-  if (sep) p.fin_on = 0;
+  const bool fin = p.fin_on != 0;
+  p.fin_on = 0;
   hipLaunchKernelGGL((ic_split_kernel<CT, TRU, MODE>), dim3(p.B * p.nbpp), dim3(kThreads), 0, st, p);
-  if (sep) hipLaunchKernelGGL(finalize_kernel, dim3(p.B), dim3(kThreads), 0, st, p.fin);
+  if (fin) hipLaunchKernelGGL(finalize_kernel, dim3(p.B), dim3(kThreads), 0, st, p.fin);
   return DPFT_OK;
 }
 
@@ -3598,14 +3285,30 @@ __global__ __launch_bounds__(kThreads) void damped_update_kernel(const float* __
 // Diagnostic streaming read (dpft_read_probe): every 16-byte word of a buffer once,
 // kProbeDepth loads in flight per lane, one float per wave written.  The measured HBM read
 // ceiling bench.py reports beside the roofline's spec peak.
-#ifndef DPFT_PROBE_GRID
-#define DPFT_PROBE_GRID 4096
-#endif
-#ifndef DPFT_PROBE_DEPTH
-#define DPFT_PROBE_DEPTH 4
-#endif
 constexpr int kProbeGrid = DPFT_PROBE_GRID;    // 16 workgroups per CU
 constexpr int kProbeDepth = DPFT_PROBE_DEPTH;  // 16-byte loads in flight per lane
+// Streaming copies for the measured copy ceiling (read + write bytes / time).  Mode 0: the
+// plain float4 copy of MI355X_MICROARCH.md's bandwidth table (one 16-byte element per thread);
+// mode 1: grid-stride, 16-byte non-temporal loads and stores, kProbeDepth in flight per lane.
+__global__ __launch_bounds__(kThreads) void copy_probe_flat_kernel(const f32x4* __restrict__ src,
+                                                                   f32x4* __restrict__ dst, size_t n4) {
+  const size_t i = (size_t)blockIdx.x * kThreads + threadIdx.x;
+  if (i < n4) dst[i] = src[i];
+}
+__global__ __launch_bounds__(kThreads) void copy_probe_kernel(const f32x4* __restrict__ src, f32x4* __restrict__ dst,
+                                                              size_t n4) {
+  const size_t stride = (size_t)gridDim.x * kThreads;
+  size_t i = (size_t)blockIdx.x * kThreads + threadIdx.x;
+  for (; i + (kProbeDepth - 1) * stride < n4; i += kProbeDepth * stride) {
+    f32x4 v[kProbeDepth];
+#pragma unroll
+    for (int k = 0; k < kProbeDepth; ++k) v[k] = __builtin_nontemporal_load(src + i + k * stride);
+#pragma unroll
+    for (int k = 0; k < kProbeDepth; ++k) __builtin_nontemporal_store(v[k], dst + i + k * stride);
+  }
+  for (; i < n4; i += stride) __builtin_nontemporal_store(__builtin_nontemporal_load(src + i), dst + i);
+}
+
 template <bool NT>
 __global__ __launch_bounds__(kThreads) void read_probe_kernel(const f32x4* __restrict__ p, size_t n4, float* out) {
   const size_t stride = (size_t)gridDim.x * kThreads;
@@ -3723,6 +3426,24 @@ int dpft_ic_damped_update(const float* jtj, const float* jtr, const float* diag_
 }
 
 size_t dpft_read_probe_out_floats(void) { return (size_t)kProbeGrid * (kThreads / 64); }
+
+int dpft_copy_probe(const void* src, void* dst, size_t bytes, int32_t mode, void* hip_stream) {
+  if (!src || !dst) return fail(DPFT_E_INVALID, "null pointer");
+  if (bytes < 16 || ((reinterpret_cast<uintptr_t>(src) | reinterpret_cast<uintptr_t>(dst)) & 15))
+    return fail(DPFT_E_INVALID, "need >= 16 bytes, 16-byte aligned");
+  const size_t n4 = bytes / 16;
+  hipStream_t st = static_cast<hipStream_t>(hip_stream);
+  const f32x4* s4 = static_cast<const f32x4*>(src);
+  f32x4* d4 = static_cast<f32x4*>(dst);
+  if (mode == 0) {
+    if (n4 > (size_t)kThreads * 0x7fffffffu) return fail(DPFT_E_INVALID, "copy too large for one flat launch");
+    hipLaunchKernelGGL(copy_probe_flat_kernel, dim3((unsigned)((n4 + kThreads - 1) / kThreads)), dim3(kThreads), 0, st,
+                       s4, d4, n4);
+  } else {
+    hipLaunchKernelGGL(copy_probe_kernel, dim3(kProbeGrid), dim3(kThreads), 0, st, s4, d4, n4);
+  }
+  return hip_check("copy_probe_kernel");
+}
 
 int dpft_read_probe(const void* buf, size_t bytes, int32_t nontemporal, float* out, void* hip_stream) {
   if (!buf || !out) return fail(DPFT_E_INVALID, "null pointer");

@@ -1,0 +1,39 @@
+// dpft_tuning.h -- the numeric operating point of libdpft_ic.so's schedules (no code paths).
+// The shipped build uses these defaults; tools/build_variants.py may override them with -D
+// for A/B builds of the SAME kernels (DESIGN.md §4 records the sweeps behind each value).
+#ifndef DPFT_TUNING_H
+#define DPFT_TUNING_H
+
+// channel-quad levels up to this many pixels per pair -> ic_split_kernel (levels 2, 3 at cfg2)
+#ifndef DPFT_SPLIT_MAX_PIXELS
+#define DPFT_SPLIT_MAX_PIXELS 40000
+#endif
+// ... and up to this many pixels per launch (all pairs of a grouped call)
+#ifndef DPFT_SPLIT_MAX_LAUNCH_PIXELS
+#define DPFT_SPLIT_MAX_LAUNCH_PIXELS 320000
+#endif
+// marching bands: weights 64 + skew / 64 - skew for the first / second dispatched half of a
+// pair's waves (swept 0..22 in rounds 1-2; 10 fastest)
+#ifndef DPFT_MARCH_SKEW
+#define DPFT_MARCH_SKEW 10
+#endif
+// marching quad loop: quads in flight (swept 2 / 3 / 4 / 6)
+#ifndef DPFT_RING_Q
+#define DPFT_RING_Q 4
+#endif
+// sigma0 / depth extrema pass: workgroups and 16-byte loads in flight per thread
+#ifndef DPFT_MM_GRID
+#define DPFT_MM_GRID 128
+#endif
+#ifndef DPFT_MM_LOADS
+#define DPFT_MM_LOADS 8
+#endif
+// diagnostic read / copy probes: workgroups (16 per CU) and 16-byte loads in flight per lane
+#ifndef DPFT_PROBE_GRID
+#define DPFT_PROBE_GRID 4096
+#endif
+#ifndef DPFT_PROBE_DEPTH
+#define DPFT_PROBE_DEPTH 4
+#endif
+
+#endif  // DPFT_TUNING_H

@@ -171,7 +171,8 @@ class LevelCall:
 
     def __init__(self, x0, x1, invD0, invD1, K, sigma0, sigma1, iters=3, remove_tru_sigma=False,
                  obj_mask0=None, obj_mask1=None, depth0=None, depth1=None, combine_icp=False,
-                 icp_weight=0.01, status=None, no_uncertainty=False, pack=False, schedule=None, weights=None):
+                 icp_weight=0.01, status=None, no_uncertainty=False, pack=False, schedule=None, weights=None,
+                 group=None):
         if not x0.is_cuda:
             raise RuntimeError("the HIP solver needs device tensors (got CPU); there is no CPU fallback")
         for name, t in (("x0", x0), ("x1", x1), ("invD0", invD0), ("invD1", invD1), ("K", K)):
@@ -230,6 +231,10 @@ class LevelCall:
         self.d0 = depth0.contiguous() if depth0 is not None else None
         self.d1 = depth1.contiguous() if depth1 is not None else None
         self.status = status if status is not None else torch.zeros(1, dtype=torch.int32, device=self.device)
+        if group is not None and group < B:  # independent batches of `group` pairs (DPFT_GROUP)
+            if group < 1 or B % group or B // group > N.GROUP_MAX_BATCHES:
+                raise ValueError(f"group={group}: B={B} must be a multiple, at most {N.GROUP_MAX_BATCHES} batches")
+            flags |= group << N.GROUP_SHIFT
         self.desc = N.LevelDesc(B, C, cs0, H, W, iters, flags, icp_weight)
         self.tens = N.LevelTensors(_ptr(self.x0), _ptr(self.x1), _ptr(self.s0), _ptr(self.s1), _ptr(self.invD0),
                                    _ptr(self.invD1), _ptr(self.d0), _ptr(self.d1), _ptr(self.m0), _ptr(self.m1),
@@ -510,18 +515,18 @@ class PyramidSolver:
         # One pose-independent pre-pass for every level's sigma0 extrema (truncated
         # sigma): each level keeps them in its own workspace slot and skips the
         # per-level min/max launch (dpft_sigma_extrema_levels, DPFT_EXTREMA_READY).
-        # Not with combine_icp (its depth1 pass shares the min/max scratch words).
+        # (combine_icp: each level's first iteration still takes its depth1 extrema and
+        # builds frame 1's normal map -- per independent batch with `group`.)
         B = self.calls[0].B
         if group is not None and group < B:
-            if group < 1 or B % group or B // group > N.GROUP_MAX_BATCHES or group >= 256:
+            if group < 1 or B % group or B // group > N.GROUP_MAX_BATCHES or group >= 4096:
                 raise ValueError(f"group={group}: B={B} must be a multiple, at most {N.GROUP_MAX_BATCHES} batches")
-            if combine_icp:
-                raise ValueError("group: not with combine_icp (its depth extrema are per call)")
             for c in self.calls:
                 c.desc.flags |= group << N.GROUP_SHIFT
         self.group = group if group is not None and group < B else B
         self.remove_tru_sigma = bool(remove_tru_sigma)
-        self.extrema_prepass = bool(remove_tru_sigma) and not combine_icp and len(self.calls) <= 4
+        self.combine_icp = bool(combine_icp)
+        self.extrema_prepass = bool(remove_tru_sigma) and len(self.calls) <= 4
         if self.extrema_prepass:
             for l, c in enumerate(self.calls):
                 c.desc.flags |= ((l + 1) << N.EXT_SLOT_SHIFT) | N.EXTREMA_READY
@@ -550,8 +555,8 @@ class PyramidSolver:
             per_level = os.environ.get("DPFT_PER_LEVEL", "0") == "1"
         L = N.lib()
         st = _stream(self.device)
-        # (truncated sigma without the one-launch extrema pre-pass -- combine_icp -- keeps
-        # the per-level minmax passes)
+        # (truncated sigma without the one-launch extrema pre-pass -- more than 4 levels --
+        # keeps the per-level minmax passes)
         if not per_level and (self.extrema_prepass or not self.remove_tru_sigma):
             n = len(self.calls)
             descs = (N.LevelDesc * n)(*[c.desc for c in reversed(self.calls)])
@@ -585,6 +590,7 @@ class PyramidSolver:
         N.check(rc, "dpft_ic_reduce_only")
 
     def algorithmic_bytes(self, level):
-        """HBM bytes one reduce launch must read: P (2C + 2Cs + 2) fp32."""
+        """HBM bytes one reduce launch must read: P (2C + 2Cs + 2) fp32, + 2 fp32 (depth0,
+        depth1) with combine_icp (272 / 280 B per pixel at C = 32, Cs = 1)."""
         d = self.calls[level].desc
-        return d.B * d.H * d.W * 4 * (2 * d.C + 2 * d.Cs + 2)
+        return d.B * d.H * d.W * 4 * (2 * d.C + 2 * d.Cs + 2 + (2 if self.combine_icp else 0))

@@ -80,7 +80,12 @@ def gather_results(R, t, jtj=None, status=None, n_pairs=None):
     split).  Each rank pads its rows to ceil(n_pairs / world) for the single
     fixed-size collective and the padding is dropped after it.  n_pairs None: equal
     shards (world * B rows)."""
-    P = pack_results(R, t, jtj, status)
+    return gather_rows(pack_results(R, t, jtj, status), n_pairs)
+
+
+def gather_rows(P, n_pairs=None):
+    """gather_results for any per-pair rows P [B, F] (fp32): this rank's shard_range
+    shard of n_pairs, all ranks' rows in pair order on every rank."""
     world, rank = dist.get_world_size(), dist.get_rank()
     B, F = P.shape
     if n_pairs is None:

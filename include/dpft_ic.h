@@ -85,15 +85,16 @@ extern "C" {
 #define DPFT_EXT_SLOT(k)    ((((uint32_t)(k)) + 1u) << DPFT_EXT_SLOT_SHIFT)
 #define DPFT_EXTREMA_READY  0x10000u
 
-/* Independent batches in one call (bits 20-27): DPFT_GROUP(n) splits the B pairs into
+/* Independent batches in one call (bits 20-31): DPFT_GROUP(n) splits the B pairs into
  * B / n consecutive batches of n pairs (B % n == 0, at most 32 batches), each solved
  * exactly as a call of its own -- its own batch-global truncated-sigma extrema
  * (algorithms.py:1975-1980) and sigma0 pre-pass -- while every launch covers all B
  * pairs (fewer, larger launches: the per-launch ramp, finish spread and finalize are
- * paid once for all batches).  0 (or n >= B): the call is one batch.  Solver entry
- * points only (not with COMBINE_ICP; the residual entry points reject it).          */
+ * paid once for all batches).  With COMBINE_ICP each batch also keeps its own depth1
+ * extrema (the normal map's invalid-depth test, algorithms.py:2168).  0 (or n >= B): the
+ * call is one batch.  Solver entry points only (the residual entry points reject it). */
 #define DPFT_GROUP_SHIFT 20
-#define DPFT_GROUP_MASK  0x0FF00000u
+#define DPFT_GROUP_MASK  0xFFF00000u
 #define DPFT_GROUP(n)    ((((uint32_t)(n)) << DPFT_GROUP_SHIFT) & DPFT_GROUP_MASK)
 
 /* device status word bits */
@@ -327,6 +328,11 @@ int dpft_ic_damped_update(const float* jtj, const float* jtr, const float* diag_
  */
 size_t dpft_read_probe_out_floats(void);
 int dpft_read_probe(const void* buf, size_t bytes, int32_t nontemporal, float* out, void* hip_stream);
+/* Diagnostic: copy `bytes` (16-byte aligned src / dst) with 16-byte loads and stores -- mode 0:
+ * one float4 per thread (MI355X_MICROARCH.md's float4 copy), mode 1: grid-stride, non-temporal,
+ * four in flight per lane; bench.py reports the faster (read + write) rate as the measured copy
+ * ceiling. */
+int dpft_copy_probe(const void* src, void* dst, size_t bytes, int32_t mode, void* hip_stream);
 
 int dpft_version(void);            /* DPFT_ABI_VERSION */
 const char* dpft_last_error(void); /* thread-local message of the last failure */

@@ -3,6 +3,7 @@
 Run in the build container only (needs /root/reference; refuses otherwise):
 
     PYTHONDONTWRITEBYTECODE=1 python tests/golden/gen_golden.py [case ...]
+    PYTHONDONTWRITEBYTECODE=1 python tests/golden/gen_golden.py --jitter case ...   (sensitivity runs)
 
 No reference code is copied: the reference package is imported read-only from
 /root/reference/code with the import shims of SURVEY.md Appendix A (stub
@@ -39,6 +40,12 @@ OPTIONS = {
     "masks_160x120_c8": dict(remove_tru_sigma=True, combine_icp=False),
     "icp_160x120_c8": dict(remove_tru_sigma=True, combine_icp=True),
     "cfg2_640x480_c32": dict(remove_tru_sigma=True, combine_icp=False),
+    "icp_640x480_c32": dict(remove_tru_sigma=True, combine_icp=True),
+    "cfg3_b8_640x480_c32": dict(remove_tru_sigma=True, combine_icp=False),
+    "cfg4_pert00_160x120_c8": dict(remove_tru_sigma=True, combine_icp=False),
+    "cfg4_pert05_160x120_c8": dict(remove_tru_sigma=True, combine_icp=False),
+    "cfg4_pert10_160x120_c8": dict(remove_tru_sigma=True, combine_icp=False),
+    "cfg4_pert20_160x120_c8": dict(remove_tru_sigma=True, combine_icp=False),
 }
 
 
@@ -145,8 +152,47 @@ def run_case(torch, A, name, dtype):
     return case, res
 
 
+JITTER_TRIALS, JITTER_ABS = 6, 1e-7
+
+
+def add_jitter(torch, A, name):
+    """The reference's own sensitivity: JITTER_TRIALS fp32 runs from the case's initial pose
+    with the translation moved by U(-1e-7, 1e-7) per coordinate (an ulp-scale change, the
+    size of the difference any other summation order makes after one step).  Appends
+    f32_jitter_R [N,B,3,3] / f32_jitter_t [N,B,3] (final poses) to the case's fixture; the
+    tests bound a chained GPU trajectory by this envelope where it exceeds 1e-4."""
+    path = os.path.join(HERE, f"{name}.npz")
+    out = dict(np.load(path, allow_pickle=False))
+    rng = np.random.default_rng(sum(ord(c) for c in name))
+    orig = recipe.make_case
+    Rs, ts = [], []
+    for _ in range(JITTER_TRIALS):
+        jit = rng.uniform(-JITTER_ABS, JITTER_ABS, size=(len(recipe.CASES[name]["pairs"]), 3)).astype(np.float32)
+
+        def jittered(**kw):
+            c = orig(**kw)
+            c["t_init"] = (c["t_init"] + jit).astype(np.float32)
+            return c
+        recipe.make_case = jittered
+        try:
+            _, res = run_case(torch, A, name, torch.float32)
+        finally:
+            recipe.make_case = orig
+        Rs.append(res["R"][-1])
+        ts.append(res["t"][-1])
+    out["f32_jitter_R"], out["f32_jitter_t"] = np.stack(Rs), np.stack(ts)
+    out["meta_jitter_abs"] = np.array(JITTER_ABS)
+    np.savez_compressed(path, **out)
+    dev = max(np.abs(out["f32_jitter_R"] - out["f32_R"][-1]).max(), np.abs(out["f32_jitter_t"] - out["f32_t"][-1]).max())
+    print(f"{name}: reference final pose moves by up to {dev:.2e} under {JITTER_ABS:g} start jitter")
+
+
 def main(names):
     torch, A = import_reference()
+    if names and names[0] == "--jitter":
+        for name in names[1:]:
+            add_jitter(torch, A, name)
+        return
     nthreads = torch.get_num_threads()
     for name in names:
         t0 = time.time()

@@ -107,8 +107,18 @@ def synthetic_weights(key, shape, gain=1.5):
     return (u * scale).astype(np.float32).reshape(shape)
 
 
+_feat_cache = {}
+
+
 def features(idx, C, level, base_down=1):
     """[C, H_l, W_l] feature stack and [1, H_l, W_l] sigma for frame idx at level."""
+    key = (idx, C, level, base_down)
+    if key not in _feat_cache:
+        _feat_cache[key] = _features(idx, C, level, base_down)
+    return _feat_cache[key]
+
+
+def _features(idx, C, level, base_down=1):
     g, npx = grey_int(idx, base_down)
     k = 1 << level
     gs = _pool_sum(g, k)
@@ -208,6 +218,36 @@ def make_case(pairs, C, levels, base_down=1, masks=False, icp=False, init=None):
     return case
 
 
+def flip_case(case, flips):
+    """Per-pair flips of every per-pixel input (code & 1: left-right, code & 2: up-down; both
+    frames of a pair alike).  Flips commute with the recipe's pooling and with the batch-
+    global invD zeroing (same value set), so a flipped pair is the recipe applied to flipped
+    frames: distinct pairs for large batches from five frames."""
+    out = dict(case)
+    for k, v in case.items():
+        if not k.startswith(INPUT_KEYS_PREFIX):
+            continue
+        a = v.copy()
+        for b, code in enumerate(flips):
+            if code & 1:
+                a[b] = a[b][..., ::-1]
+            if code & 2:
+                a[b] = a[b][..., ::-1, :]
+        out[k] = np.ascontiguousarray(a)
+    return out
+
+
+def sweep_case(B, C=8, levels=4, base_down=4, masks=True):
+    """cfg4's batch: B pairs cycled through the 20 ordered pairs of the five frames, each
+    round of 20 with its own flip code (80 distinct pairs), object masks = depth below the
+    frame's median, identity initial pose."""
+    pairs = [ORDERED_PAIRS[k % len(ORDERED_PAIRS)] for k in range(B)]
+    flips = [(k // len(ORDERED_PAIRS)) % 4 for k in range(B)]
+    case = flip_case(make_case(pairs, C, levels, base_down, masks=masks), flips)
+    case["flips"] = np.array(flips, np.int32)
+    return case
+
+
 INPUT_KEYS_PREFIX = ("x0_", "x1_", "s0_", "s1_", "invD0_", "invD1_", "depth0_", "depth1_", "mask0_", "mask1_")
 
 
@@ -219,6 +259,22 @@ def input_digests(case):
             out[k] = hashlib.sha256(a.tobytes()).hexdigest()
     return out
 
+
+def perturbations(n, rot, trs, k0=0):
+    """n deterministic (so3 vector, translation) starts of magnitude rot rad / trs m:
+    integer direction triples rotated through a fixed table (cfg4's large-baseline
+    starts, applied as the solver-level initial pose)."""
+    dirs = [(1, -2, 1), (-1, 1, 2), (2, 1, -1), (-2, -1, -1), (1, 2, 2), (-1, -2, 1), (2, -1, 2)]
+    out = []
+    for i in range(n):
+        a = np.array(dirs[(i + k0) % len(dirs)], np.float64)
+        b = np.array(dirs[(i + k0 + 3) % len(dirs)], np.float64)
+        out.append(((rot * a / np.sqrt((a * a).sum())).tolist(), (trs * b / np.sqrt((b * b).sum())).tolist()))
+    return out
+
+
+ORDERED_PAIRS = [(i, j) for i in range(5) for j in range(5) if i != j]  # cfg3's 20 ordered pairs
+CFG4_PAIRS = [(0, 1), (1, 3), (2, 4), (4, 0)]
 
 # Named cases shared by the fixture generator and the tests.
 CASES = {
@@ -236,4 +292,18 @@ CASES = {
     "icp_160x120_c8": dict(pairs=[(0, 2)], C=8, levels=2, base_down=4, icp=True),
     # cfg2: 640x480, C=32, 4 levels
     "cfg2_640x480_c32": dict(pairs=[(0, 1)], C=32, levels=4, base_down=1),
+    # cfg5: cfg2's inputs + combine_ICP (ICP weight 0.01) at full size
+    "icp_640x480_c32": dict(pairs=[(0, 1)], C=32, levels=4, base_down=1, icp=True),
+    # cfg3: the bench's first batch -- 8 distinct ordered pairs at 640x480, C=32, 4 levels
+    # (batch-global truncated-sigma extrema over different pairs)
+    "cfg3_b8_640x480_c32": dict(pairs=ORDERED_PAIRS[:8], C=32, levels=4, base_down=1),
+    # cfg4: object masks, 4 levels at 160x120, C=8, large-baseline initial poses (three start
+    # sets of growing magnitude; each one reference call over the 4 pairs)
+    "cfg4_pert00_160x120_c8": dict(pairs=CFG4_PAIRS, C=8, levels=4, base_down=4, masks=True),  # identity start
+    "cfg4_pert05_160x120_c8": dict(pairs=CFG4_PAIRS, C=8, levels=4, base_down=4, masks=True,
+                                   init=perturbations(4, 0.05, 0.05, 0)),
+    "cfg4_pert10_160x120_c8": dict(pairs=CFG4_PAIRS, C=8, levels=4, base_down=4, masks=True,
+                                   init=perturbations(4, 0.10, 0.10, 1)),
+    "cfg4_pert20_160x120_c8": dict(pairs=CFG4_PAIRS, C=8, levels=4, base_down=4, masks=True,
+                                   init=perturbations(4, 0.20, 0.15, 2)),
 }

@@ -36,8 +36,9 @@ def test_invalid_descriptor_is_rejected_without_device_work():
 
 
 def test_group_descriptor_validation_without_device_work():
-    """DPFT_GROUP(n): B a multiple of n, at most 32 batches, not with COMBINE_ICP; n >= B
-    (or 0) is one batch.  Checked by the descriptor validation every entry point runs."""
+    """DPFT_GROUP(n): B a multiple of n, at most 32 batches (COMBINE_ICP too: per-batch
+    depth1 extrema); n >= B (or 0) is one batch; n up to 2048 (a 12-bit field).  Checked by
+    the descriptor validation every entry point runs."""
     import ctypes
     L = N.lib()
     G = lambda n: n << N.GROUP_SHIFT
@@ -50,4 +51,6 @@ def test_group_descriptor_validation_without_device_work():
     assert ws(12, base | G(8)) == 0                                        # not a multiple
     assert b"DPFT_GROUP" in L.dpft_last_error()
     assert ws(64, base | G(1)) == 0                                        # 64 batches > 32
-    assert ws(32, N.REMOVE_TRU_SIGMA | N.COMBINE_ICP | G(8)) == 0          # ICP: per-call depth extrema
+    assert ws(32, N.REMOVE_TRU_SIGMA | N.COMBINE_ICP | G(8)) > 0           # ICP: per-batch depth extrema
+    assert ws(2048, base | G(256)) > 0 and ws(2048, base | G(256)) == ws(2048, base)  # 8 batches of 256
+    assert ws(2048, base | G(1024)) > 0

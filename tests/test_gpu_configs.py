@@ -1,0 +1,374 @@
+"""BASELINE.json configurations 3, 4 and 5 on a real MI355X (`-m gpu`), against fixtures the
+reference itself produced (tests/golden/gen_golden.py).
+
+* cfg5 -- joint feature-metric + ICP (combine_ICP, weight 0.01) at 640x480, C = 32, 4 levels:
+  the whole solve, every iteration restarted from the reference's pose, and independent
+  batches in one call (DPFT_GROUP: per-batch depth1 extrema for the normal map).
+* cfg3 -- the bench's first batch: 8 distinct ordered pairs at 640x480, C = 32, so the
+  batch-global truncated-sigma extrema (algorithms.py:1975-1980) span different pairs; one
+  call and the grouped launch of the bench (every batch solved as its own call).
+* cfg4 -- object masks, 4 levels at 160x120, C = 8, large-baseline starts applied as the
+  solver-level initial pose (three start sets + the identity start), and the B = 256 sweep
+  of convergence_basin.solve_from_starts against the oracle and against separate calls.
+
+Tolerances: se(3) 1e-4 against the fp32 and fp64 reference runs (BASELINE.json); invalid-
+pixel counts exact when an iteration starts from the reference's own pose.
+"""
+import numpy as np
+import pytest
+import torch
+
+import golden_io
+import recipe
+
+pytestmark = pytest.mark.gpu
+
+SE3_TOL = 1e-4
+
+
+def _dev():
+    if not torch.cuda.is_available():
+        pytest.skip("no HIP device")
+    return torch.device("cuda:0")
+
+
+def _solver_levels(case, dev, pack):
+    """Per-level PyramidSolver dicts of a recipe case (features packed to channel quads when
+    `pack`)."""
+    from deep_prob_feature_track_amd import ic
+    out = []
+    for d in golden_io.levels_torch(case, torch.float32, dev):
+        e = dict(x0=ic.pack_features(d["f0"]) if pack else d["f0"], x1=ic.pack_features(d["f1"]) if pack else d["f1"],
+                 invD0=d["invD0"], invD1=d["invD1"], sigma0=d["s0"], sigma1=d["s1"])
+        for k in ("depth0", "depth1"):
+            if k in d:
+                e[k] = d[k]
+        if "mask0" in d:
+            e["obj_mask0"], e["obj_mask1"] = d["mask0"], d["mask1"]
+        out.append(e)
+    return out
+
+
+def _assert_on_reference(R, t, z, i=-1, tol=SE3_TOL, what="", precs=("f32", "f64")):
+    R = R.cpu().numpy().reshape(-1, 3, 3)
+    t = t.cpu().numpy().reshape(-1, 3)
+    for prec in precs:
+        if f"{prec}_R" in z:
+            dR = np.abs(R - z[f"{prec}_R"][i]).max()
+            dt = np.abs(t - z[f"{prec}_t"][i]).max()
+            assert dR <= tol and dt <= tol, f"{what} vs {prec} reference: |dR| {dR:.2e} |dt| {dt:.2e}"
+
+
+def jitter_envelope(z):
+    """Per pair, how far the reference's own final pose moves when its start pose moves by
+    1e-7 (tests/golden/gen_golden.py --jitter: six fp32 runs): max over the runs of
+    max(|dR|, |dt|) against the unjittered run."""
+    dR = np.abs(z["f32_jitter_R"] - z["f32_R"][-1][None]).max(axis=(2, 3))
+    dt = np.abs(z["f32_jitter_t"] - z["f32_t"][-1][None]).max(axis=2)
+    return np.maximum(dR, dt).max(axis=0)
+
+
+def _assert_within_reference_envelope(R, t, z, what=""):
+    """The chained final pose against the reference's fp32 run: within 1e-4 or, where the
+    reference itself is more sensitive than that, within twice its own 1e-7-jitter
+    envelope (a chained trajectory differs from the reference's by ulp-scale steps, and the
+    batch-global masks turn some ulp changes into jumps -- the reference's own jitter runs
+    show the size of those jumps).  The restart tests pin every iteration exactly."""
+    env = jitter_envelope(z)
+    R = R.cpu().numpy().reshape(-1, 3, 3)
+    t = t.cpu().numpy().reshape(-1, 3)
+    dev = np.maximum(np.abs(R - z["f32_R"][-1]).max(axis=(1, 2)), np.abs(t - z["f32_t"][-1]).max(axis=1))
+    bound = np.maximum(SE3_TOL, 2.0 * env)
+    assert (dev <= bound).all(), f"{what}: deviation {dev} vs bound {bound} (reference envelope {env})"
+    return dev, env
+
+
+def _restart_iterations(name, dev, pack, **extra):
+    """Every iteration from the reference's pose of the previous one: exact invalid counts,
+    normal equations and the updated pose to rounding."""
+    from deep_prob_feature_track_amd import ic
+    case, z = golden_io.load(name)
+    lv = golden_io.levels_torch(case, torch.float32, dev)
+    R0, t0 = golden_io.init_pose(case, torch.float32, dev)
+    K = torch.from_numpy(case["K"]).to(dev)
+    L, i = case["levels"], 0
+    for l in reversed(range(L)):
+        d = lv[l]
+        f0, f1 = (ic.pack_features(d["f0"]), ic.pack_features(d["f1"])) if pack else (d["f0"], d["f1"])
+        for it in range(3):
+            R = torch.from_numpy(z["f32_R"][i - 1]).to(dev) if i else R0
+            t = (torch.from_numpy(z["f32_t"][i - 1]).to(dev) if i else t0).reshape(-1, 3, 1)
+            Rn, tn, jtj, jtr, inv = ic.iterate(
+                (R, t), f0, f1, d["invD0"], d["invD1"], K / 2 ** l, d["s0"], d["s1"], first=True,
+                reverse=(it & 1) == 1, remove_tru_sigma=bool(z["opt_remove_tru_sigma"]), obj_mask0=d.get("mask0"),
+                obj_mask1=d.get("mask1"), depth0=d.get("depth0"), depth1=d.get("depth1"),
+                combine_icp=bool(z["opt_combine_icp"]), **extra)
+            inv = inv.cpu().numpy()
+            assert np.array_equal(inv, z["f32_invalid"][i]), f"{name} iter {i}: {inv} vs {z['f32_invalid'][i]}"
+            ref_j, ref_r = z["f32_jtj"][i], z["f32_jtr"][i]
+            assert np.abs(jtj.cpu().numpy() - ref_j).max() / np.abs(ref_j).max() < 1e-5, f"iter {i} JtJ"
+            assert np.abs(jtr.cpu().numpy() - ref_r).max() / np.abs(ref_r).max() < 1e-4, f"iter {i} JtR"
+            # one step from the fp32 run's pose: against that run's next pose
+            _assert_on_reference(Rn, tn, z, i, tol=2e-5, what=f"{name} iter {i} (one step)", precs=("f32",))
+            i += 1
+
+
+# ------------------------------------------------------------------------------ cfg5
+@pytest.mark.parametrize("pack", [True, False])
+def test_cfg5_icp_full_size_solve(pack):
+    """combine_ICP at 640x480, C = 32: the 4-level solve (one dpft_ic_solve_pyramid call:
+    the sigma0 extrema pre-pass, each level's depth1 extrema and normal map) lands on the
+    reference's fp32 and fp64 poses, and equals the per-level calls bit for bit."""
+    from deep_prob_feature_track_amd import ic
+    dev = _dev()
+    case, z = golden_io.load("icp_640x480_c32")
+    solver = ic.PyramidSolver(_solver_levels(case, dev, pack), torch.from_numpy(case["K"]).to(dev), iters=3,
+                              remove_tru_sigma=True, combine_icp=True)
+    assert solver.extrema_prepass
+    R0, t0 = golden_io.init_pose(case, torch.float32, dev)
+    outs = []
+    for per_level in (False, True):
+        R, t = R0.clone().contiguous(), t0.reshape(-1, 3).clone().contiguous()
+        solver.run(R, t, per_level=per_level)
+        torch.cuda.synchronize()
+        ic.check_status(solver.status)
+        outs.append((R, t))
+    assert torch.equal(outs[0][0], outs[1][0]) and torch.equal(outs[0][1], outs[1][1])
+    _assert_on_reference(*outs[0], z, what="cfg5 final")
+    # the epe between the two reference precisions bounds what 1e-4 means here
+    assert np.abs(z["f32_t"][-1] - z["f64_t"][-1]).max() < SE3_TOL
+
+
+@pytest.mark.parametrize("pack", [True, False])
+def test_cfg5_icp_iterations_from_reference_pose(pack):
+    _restart_iterations("icp_640x480_c32", _dev(), pack)
+
+
+def test_cfg5_grouped_icp_batches_solve_as_separate_calls():
+    """Independent batches with combine_ICP in one call: batch g's depths scaled by
+    1 + g / 8 (inverse depths by its inverse), so each batch has its own depth1 extrema
+    and the normal map must zero its own (algorithms.py:2168 over the batch one reference
+    call holds).  Grouped = separate calls: JtJ of a no-update iteration at every level
+    (the ICP term included) and the solved poses."""
+    from deep_prob_feature_track_amd import ic
+    dev = _dev()
+    case, z = golden_io.load("icp_640x480_c32")
+    G, B = 4, 2
+    n = G * B
+    base = _solver_levels(case, dev, True)
+    scale = (1.0 + torch.arange(G, device=dev, dtype=torch.float32) / 8).repeat_interleave(B).view(n, 1, 1, 1)
+    rep = lambda x: x.repeat(n, *([1] * (x.dim() - 1)))
+    levels = []
+    for d in base:
+        e = {k: rep(v) for k, v in d.items()}
+        for k in ("depth0", "depth1"):
+            e[k] = (e[k] * scale).contiguous()
+        for k in ("invD0", "invD1"):
+            e[k] = (e[k] / scale).contiguous()
+        levels.append(e)
+    K = rep(torch.from_numpy(case["K"]).to(dev))
+    R0, t0 = golden_io.init_pose(case, torch.float32, dev)
+    R0, t0 = rep(R0).contiguous(), rep(t0.reshape(-1, 3)).clone()
+    t0[:, 1] += 1e-3 * (torch.arange(n, device=dev, dtype=torch.float32) % B)
+    grouped = ic.PyramidSolver(levels, K, iters=3, remove_tru_sigma=True, combine_icp=True, group=B)
+    Rg, tg = R0.clone(), t0.clone()
+    grouped.run(Rg, tg)
+    torch.cuda.synchronize()
+    ic.check_status(grouped.status)
+    sl = lambda g: slice(g * B, (g + 1) * B)
+    for g in range(G):
+        lv_g = [{k: v[sl(g)] for k, v in d.items()} for d in levels]
+        alone = ic.PyramidSolver(lv_g, K[sl(g)].contiguous(), iters=3, remove_tru_sigma=True, combine_icp=True)
+        Ra, ta = R0[sl(g)].clone(), t0[sl(g)].clone()
+        alone.run(Ra, ta)
+        torch.cuda.synchronize()
+        torch.testing.assert_close(Rg[sl(g)], Ra, rtol=0, atol=5e-5)
+        torch.testing.assert_close(tg[sl(g)], ta, rtol=0, atol=5e-5)
+        for l in range(len(levels)):  # normal equations at the same pose, ICP term included
+            dg, da = levels[l], lv_g[l]
+            kw = dict(first=True, update=False, remove_tru_sigma=True, combine_icp=True)
+            pose = (Ra, ta.view(-1, 3, 1))
+            a = ic.iterate(pose, da["x0"], da["x1"], da["invD0"], da["invD1"], K[sl(g)] / 2 ** l, da["sigma0"],
+                           da["sigma1"], depth0=da["depth0"], depth1=da["depth1"], **kw)
+            # the grouped call over every batch (only batch g's rows compared)
+            Rall, tall = Rg.clone(), tg.clone().view(-1, 3, 1)
+            Rall[sl(g)], tall[sl(g)] = Ra, ta.view(-1, 3, 1)
+            b = ic.iterate((Rall, tall), dg["x0"], dg["x1"], dg["invD0"], dg["invD1"], K / 2 ** l, dg["sigma0"],
+                           dg["sigma1"], depth0=dg["depth0"], depth1=dg["depth1"], group=B, **kw)
+            assert torch.equal(a[4], b[4][sl(g)]), f"batch {g} level {l} invalid counts"
+            torch.testing.assert_close(b[2][sl(g)], a[2], rtol=2e-6, atol=1e-6 * a[2].abs().max().item())
+
+
+# ------------------------------------------------------------------------------ cfg3
+@pytest.mark.parametrize("groups", [0, 16])
+def test_cfg3_distinct_pairs_match_reference(groups):
+    """8 distinct pairs in one call (groups = 0), and the bench's launch: 16 batches of the
+    same 8 pairs in one grouped call, every batch solved as its own reference call -- R and
+    t of every pair within 1e-4 of the fp32 and fp64 reference runs of the 8-pair batch."""
+    from deep_prob_feature_track_amd import ic
+    dev = _dev()
+    case, z = golden_io.load("cfg3_b8_640x480_c32")
+    G = max(1, groups)
+    B = case["B"]
+    rep = lambda x: x.repeat(G, *([1] * (x.dim() - 1))) if G > 1 else x
+    levels = [{k: rep(v) for k, v in d.items()} for d in _solver_levels(case, dev, True)]
+    solver = ic.PyramidSolver(levels, rep(torch.from_numpy(case["K"]).to(dev)), iters=3, remove_tru_sigma=True,
+                              group=B if G > 1 else None)
+    R0, t0 = golden_io.init_pose(case, torch.float32, dev)
+    R, t = rep(R0).contiguous(), rep(t0.reshape(-1, 3)).contiguous()
+    solver.run(R, t)
+    torch.cuda.synchronize()
+    ic.check_status(solver.status)
+    for g in range(G):
+        _assert_on_reference(R[g * B:(g + 1) * B], t[g * B:(g + 1) * B], z, what=f"cfg3 batch {g}")
+
+
+@pytest.mark.parametrize("pack", [True, False])
+def test_cfg3_iterations_from_reference_pose(pack):
+    _restart_iterations("cfg3_b8_640x480_c32", _dev(), pack)
+
+
+def test_cfg3_grouped_iterations_from_reference_pose():
+    """The grouped launch (2 batches of the 8 distinct pairs) restarted from the reference's
+    poses: each batch's invalid counts equal the reference's exactly."""
+    from deep_prob_feature_track_amd import ic
+    dev = _dev()
+    case, z = golden_io.load("cfg3_b8_640x480_c32")
+    lv = golden_io.levels_torch(case, torch.float32, dev)
+    K = torch.from_numpy(case["K"]).to(dev)
+    B, G = case["B"], 2
+    rep = lambda x: x.repeat(G, *([1] * (x.dim() - 1)))
+    L, i = case["levels"], 0
+    for l in reversed(range(L)):
+        d = lv[l]
+        f0, f1 = rep(ic.pack_features(d["f0"])), rep(ic.pack_features(d["f1"]))
+        for it in range(3):
+            if i == 0:
+                R, t = golden_io.init_pose(case, torch.float32, dev)
+            else:
+                R, t = torch.from_numpy(z["f32_R"][i - 1]).to(dev), torch.from_numpy(z["f32_t"][i - 1]).to(dev)
+            o = ic.iterate((rep(R), rep(t.reshape(-1, 3, 1))), f0, f1, rep(d["invD0"]), rep(d["invD1"]),
+                           rep(K) / 2 ** l, rep(d["s0"]), rep(d["s1"]), first=True, remove_tru_sigma=True, group=B)
+            inv = o[4].cpu().numpy()
+            for g in range(G):
+                assert np.array_equal(inv[g * B:(g + 1) * B], z["f32_invalid"][i]), f"iter {i} batch {g}"
+            i += 1
+
+
+# ------------------------------------------------------------------------------ cfg4
+CFG4 = ["cfg4_pert00_160x120_c8", "cfg4_pert05_160x120_c8", "cfg4_pert10_160x120_c8", "cfg4_pert20_160x120_c8"]
+
+
+@pytest.mark.parametrize("name", CFG4)
+@pytest.mark.parametrize("pack", [True, False])
+def test_cfg4_solve_from_perturbed_start(name, pack):
+    """Masks, 4 levels at 160x120, C = 8, from the fixture's start.  Every iteration
+    restarted from the reference's pose gives its invalid counts exactly and its next pose
+    to 2e-5 (measured 6e-8); the chained solve ends within the reference's own sensitivity
+    envelope (measured: the reference moves by up to 2.4e-3 under a 1e-7 start change on
+    these masked cases; the GPU's chained deviation 2.4e-4 .. 4.6e-4)."""
+    from deep_prob_feature_track_amd import convergence_basin as cb
+    dev = _dev()
+    case, z = golden_io.load(name)
+    _restart_iterations(name, dev, pack)
+    R0, t0 = golden_io.init_pose(case, torch.float32, dev)
+    R, t = cb.solve_from_starts(_solver_levels(case, dev, pack), torch.from_numpy(case["K"]).to(dev), R0[None],
+                                t0[None])
+    _assert_within_reference_envelope(R[0], t[0], z, what=name)
+
+
+def test_cfg4_start_sets_in_one_grouped_call():
+    """The four fixture start sets as four independent batches of one call
+    (solve_from_starts): each equals its reference run, and the convergence counts against
+    the identity-start solve equal those of the reference's own final poses wherever the
+    margins exceed the pose tolerance."""
+    from deep_prob_feature_track_amd import convergence_basin as cb
+    dev = _dev()
+    zs = [golden_io.load(n) for n in CFG4]
+    case = zs[0][0]
+    R0 = torch.stack([golden_io.init_pose(c, torch.float32, dev)[0] for c, _ in zs])
+    t0 = torch.stack([golden_io.init_pose(c, torch.float32, dev)[1] for c, _ in zs])
+    R, t = cb.solve_from_starts(_solver_levels(case, dev, True), torch.from_numpy(case["K"]).to(dev), R0, t0)
+    envs = []
+    for p, (_, z) in enumerate(zs):
+        envs.append(_assert_within_reference_envelope(R[p], t[p], z, what=CFG4[p])[1])
+    ref_R = torch.from_numpy(np.stack([z["f32_R"][-1] for _, z in zs])).to(dev)
+    ref_t = torch.from_numpy(np.stack([z["f32_t"][-1] for _, z in zs])).to(dev)
+    n_gpu, m_gpu = cb.basin_counts(R, t, R[0], t[0], rot_thresh=0.02, trans_thresh=0.02)
+    n_ref, m_ref = cb.basin_counts(ref_R, ref_t, ref_R[0], ref_t[0], rot_thresh=0.02, trans_thresh=0.02)
+    # a count is decided where every margin exceeds the pose uncertainty (the reference's own
+    # envelope of the start set and of the identity start, twice): those pairs must agree
+    unc = 2.0 * (np.stack(envs) + np.stack(envs)[:1])
+    sure = (np.abs(m_ref["rot_margin"]) > unc) & (np.abs(m_ref["trans_margin"]) > unc)
+    conv_g = (m_gpu["rot_margin"] > 0) & (m_gpu["trans_margin"] > 0)
+    conv_r = (m_ref["rot_margin"] > 0) & (m_ref["trans_margin"] > 0)
+    assert np.array_equal(conv_g[sure], conv_r[sure]), f"counts {n_gpu} vs reference {n_ref}"
+    assert n_gpu[0] == case["B"]
+    print("cfg4 fixture starts: convergence counts (GPU / reference):", n_gpu.tolist(), n_ref.tolist(),
+          "decided pairs:", sure.sum(1).tolist())
+
+
+def test_cfg4_sweep_b256():
+    """cfg4's batch: 256 masked pairs at 160x120, C = 8 (tests/golden/recipe.py sweep_case).
+    The identity-start solve (the basin's target) against the oracle on the same 256-pair
+    batch: level 0's last iteration restarted from the oracle's pose gives the oracle's
+    invalid counts exactly, and the chained poses lie within the oracle's own envelope under
+    a 1e-7 start change (three jittered oracle runs).  Then a 1-D sweep of perturbed starts
+    around the target (6 axes x 5 offsets up to 0.2 rad / 0.15 m: 30 start sets = 7680
+    solves in grouped calls of 8 start sets): start sets solved in one grouped call equal the
+    same sets solved one call each, and the convergence counts are reported with the number
+    of pairs whose margin is below the pose uncertainty."""
+    from deep_prob_feature_track_amd import convergence_basin as cb
+    from deep_prob_feature_track_amd import ic
+    from oracle import ic_oracle as O
+    dev = _dev()
+    case = recipe.sweep_case(256)
+    B = case["B"]
+    K = torch.from_numpy(case["K"]).to(dev)
+    lv = _solver_levels(case, dev, True)
+    I = torch.eye(3, device=dev).repeat(1, B, 1, 1)
+    Rt, tt = cb.solve_from_starts(lv, K, I, torch.zeros(1, B, 3, device=dev))
+    Rt, tt = Rt[0], tt[0]
+    # the oracle on the same batch (batch-global extrema over all 256 pairs), plain and jittered
+    lc = golden_io.levels_torch(case, torch.float32)
+    Kc = torch.from_numpy(case["K"])
+    g = torch.Generator().manual_seed(4)
+    runs, trace = [], []
+    with torch.no_grad():
+        for k in range(4):
+            t0 = torch.zeros(B, 3, 1) if k == 0 else (torch.rand(B, 3, 1, generator=g) * 2 - 1) * 1e-7
+            runs.append(O.solve_pyramid(torch.eye(3).repeat(B, 1, 1), t0, lc, Kc, iters=3, remove_tru_sigma=True,
+                                        trace=trace if k == 0 else None))
+    Ro, to = runs[0][0], runs[0][1].view(B, 3)
+    env = torch.stack([torch.maximum((r - Ro).abs().amax((1, 2)), (t.view(B, 3) - to).abs().amax(1))
+                       for r, t in runs[1:]]).amax(0)
+    dev_pose = torch.maximum((Rt.cpu() - Ro).abs().amax((1, 2)), (tt.cpu() - to).abs().amax(1))
+    bound = torch.clamp(2.0 * env, min=SE3_TOL)
+    assert (dev_pose <= bound).all(), f"{int((dev_pose > bound).sum())} pairs outside the oracle's envelope"
+    print(f"cfg4 B=256 identity start vs oracle: {int((dev_pose <= SE3_TOL).sum())} of {B} pairs within 1e-4, "
+          f"max {dev_pose.max().item():.2e} (oracle envelope max {env.max().item():.2e})")
+    # level 0's last iteration from the oracle's own pose: exact invalid counts
+    d = lv[0]
+    it = trace[-2]
+    o = ic.iterate((it["R"].to(dev), it["t"].to(dev).view(B, 3, 1)), d["x0"], d["x1"], d["invD0"], d["invD1"], K,
+                   d["sigma0"], d["sigma1"], first=True, reverse=False, remove_tru_sigma=True,
+                   obj_mask0=d["obj_mask0"], obj_mask1=d["obj_mask1"])
+    assert np.array_equal(o[4].cpu().numpy(), trace[-1]["invalid"].numpy())
+    jr = trace[-1]["JtJ"].numpy()
+    assert np.abs(o[2].cpu().numpy() - jr).max() / np.abs(jr).max() < 1e-5
+    # the sweep
+    rot = np.linspace(-0.2, 0.2, 5)
+    trs = np.linspace(-0.15, 0.15, 5)
+    Rs, ts = cb.perturbed_starts(Rt, tt, rot, trs)
+    assert Rs.shape[:2] == (30, B)
+    Rf, tf = cb.solve_from_starts(lv, K, Rs, ts)
+    for p in (0, 13, 29):  # grouped = one call per start set (summation grouping only)
+        Ra, ta = cb.solve_from_starts(lv, K, Rs[p:p + 1], ts[p:p + 1])
+        close = torch.maximum((Rf[p] - Ra[0]).abs().amax((1, 2)), (tf[p] - ta[0]).abs().amax(1))
+        assert (close.cpu() <= bound).all(), f"start set {p}: grouped vs alone {close.max().item():.2e}"
+    counts, m = cb.basin_counts(Rf, tf, Rt, tt, rot_thresh=0.01, trans_thresh=0.01)
+    unc = bound.numpy()[None]
+    near = (np.abs(m["rot_margin"]) < unc) | (np.abs(m["trans_margin"]) < unc)
+    assert all(counts[a * 5 + 2] >= B - near[a * 5 + 2].sum() for a in range(6))  # zero-offset starts
+    print("cfg4 sweep counts (6 axes x 5 offsets):", counts.reshape(6, 5).tolist(),
+          "undecided (margin < uncertainty):", near.sum(1).reshape(6, 5).tolist())

@@ -16,6 +16,7 @@ import recipe
 from oracle import ic_oracle as O
 
 CASES = list(recipe.CASES)
+SLOW_F64 = {"cfg3_b8_640x480_c32"}  # ~35 s per fp64 oracle run on 8 CPU threads
 
 
 def run_oracle(name, dtype):
@@ -45,13 +46,18 @@ def test_oracle_matches_reference(name, prec):
     2.6e-5 (fp32); the se(3) acceptance bound is 1e-4 (BASELINE.json).
     """
     dtype = torch.float64 if prec == "f64" else torch.float32
+    if name in SLOW_F64 and prec == "f64":
+        pytest.skip("8 pairs at 640x480 in fp64: covered by the restarted-iteration test")
     case, z, trace = run_oracle(name, dtype)
     if f"{prec}_R" not in z:
         pytest.skip(f"reference cannot run {prec} for {name}")
     assert len(trace) == z[f"{prec}_R"].shape[0] == 3 * case["levels"]   # fixed 3 iterations per level
     fragile = bool(z["opt_remove_tru_sigma"])
-    tight = 1e-12 if prec == "f64" else 1e-8
-    loose = (2e-5 if prec == "f64" else 5e-5) if fragile else tight
+    tight = 1e-12 if prec == "f64" else 1e-7  # fp32 iteration 0: summation order only (measured 3.4e-8)
+    # chained fp32: the reference's own fp32 trajectory moves by up to 9.7e-5 against
+    # its fp64 one (SURVEY.md App. B); measured worst here 8.9e-5 (cfg4_pert20)
+    loose = (2e-5 if prec == "f64" else 1e-4) if fragile else tight
+    L = case["levels"]
     for i, tr in enumerate(trace):
         dR = np.abs(tr["R"].numpy() - z[f"{prec}_R"][i]).max()
         dt = np.abs(tr["t"].numpy() - z[f"{prec}_t"][i]).max()
@@ -61,8 +67,48 @@ def test_oracle_matches_reference(name, prec):
         rel = np.abs(tr["JtJ"].numpy() - jtj_ref).max() / np.abs(jtj_ref).max()
         assert rel <= (1e-4 if (fragile and i > 0) else (1e-10 if prec == "f64" else 1e-5)), \
             f"{name} {prec} iter {i}: JtJ rel {rel:.3e}"
+        # Chained, the invalid set drifts with the pose noise (the truncated-sigma equality
+        # tests flip pixels under 1e-5 pose changes: measured up to 0.4 % of a level's
+        # pixels); the restarted test below proves the counts exact from the same pose.
         dinv = np.abs(tr["invalid"].numpy() - z[f"{prec}_invalid"][i]).max()
-        assert dinv == 0 if (i == 0 or not fragile) else dinv <= 1000
+        npx = case[f"invD0_{L - 1 - i // 3}"][0].size
+        assert dinv == 0 if (i == 0 or not fragile) else dinv <= 0.01 * npx, f"iter {i}: {dinv} of {npx}"
+
+
+@pytest.mark.parametrize("name", CASES)
+@pytest.mark.parametrize("prec", ["f64", "f32"])
+def test_oracle_restarted_iterations_exact(name, prec):
+    """Every iteration restarted from the reference's own pose of the previous iteration
+    (the initial pose for the first): the invalid-pixel count equals the reference's
+    EXACTLY (integer work), the normal equations and the updated pose agree to rounding.
+    Measured worst over the fixtures: JtJ rel 4.3e-6 / 8e-15, JtR rel 6.5e-6 / 2.1e-14,
+    pose 3.4e-8 / 6.4e-18 (fp32 / fp64)."""
+    dtype = torch.float64 if prec == "f64" else torch.float32
+    case, z = golden_io.load(name)
+    if f"{prec}_R" not in z:
+        pytest.skip(f"reference cannot run {prec} for {name}")
+    lv = golden_io.levels_torch(case, dtype)
+    R0, t0 = golden_io.init_pose(case, dtype)
+    K = torch.from_numpy(case["K"]).to(dtype)
+    L = case["levels"]
+    f64 = prec == "f64"
+    for i in range(3 * L):
+        l = L - 1 - i // 3
+        R = torch.from_numpy(z[f"{prec}_R"][i - 1]).to(dtype) if i else R0
+        t = torch.from_numpy(z[f"{prec}_t"][i - 1]).to(dtype) if i else t0
+        d, tr = lv[l], []
+        with torch.no_grad():
+            O.solve_level(R, t, d["f0"], d["f1"], d["s0"], d["s1"], d["invD0"], d["invD1"], K / 2 ** l, iters=1,
+                          remove_tru_sigma=bool(z["opt_remove_tru_sigma"]), mask0=d.get("mask0"),
+                          mask1=d.get("mask1"), depth0=d.get("depth0"), depth1=d.get("depth1"),
+                          icp_scale=0.01 if bool(z["opt_combine_icp"]) else None, trace=tr)
+        x = tr[0]
+        assert np.array_equal(x["invalid"].numpy(), z[f"{prec}_invalid"][i]), f"{name} {prec} iter {i}"
+        jtj, jtr = z[f"{prec}_jtj"][i], z[f"{prec}_jtr"][i]
+        assert np.abs(x["JtJ"].numpy() - jtj).max() / np.abs(jtj).max() <= (1e-13 if f64 else 2e-5), f"iter {i}"
+        assert np.abs(x["JtR"].numpy() - jtr).max() / np.abs(jtr).max() <= (1e-12 if f64 else 5e-5), f"iter {i}"
+        for k in ("R", "t"):
+            assert np.abs(x[k].numpy() - z[f"{prec}_{k}"][i]).max() <= (1e-15 if f64 else 1e-6), f"iter {i} {k}"
 
 
 @pytest.mark.parametrize("name", ["cfg1_160x120_c8", "batch4_160x120_c8", "masks_160x120_c8", "icp_160x120_c8"])

@@ -3,6 +3,10 @@
 tools/variant_pytest.py honour it).
 
 python tools/build_variants.py name=-DFLAG=V[,-DFLAG2=V] ...
+
+The shipped source has no alternative code paths; a variant only moves the numeric operating
+point of csrc/dpft_tuning.h (DPFT_SPLIT_MAX_PIXELS, DPFT_SPLIT_MAX_LAUNCH_PIXELS,
+DPFT_MARCH_SKEW, DPFT_RING_Q, DPFT_MM_GRID, DPFT_MM_LOADS, DPFT_PROBE_GRID, DPFT_PROBE_DEPTH).
 """
 import os
 import subprocess
@@ -18,7 +22,7 @@ def one(spec):
     name, flags = spec.split("=", 1)
     out = os.path.join(ROOT, "tools", "libs", f"libdpft_{name}.so")
     os.makedirs(os.path.dirname(out), exist_ok=True)
-    cmd = [B.HIPCC, f"--offload-arch={B.ARCH}", "-O3", "-std=c++17", "-shared", "-fPIC", f"-I{B.INC}",
+    cmd = [B.HIPCC, f"--offload-arch={B.ARCH}", "-O3", "-std=c++17", "-shared", "-fPIC", f"-I{B.INC}", f"-I{os.path.dirname(B.SRC)}",
            *[f for f in flags.split(",") if f], "-o", out, B.SRC]
     subprocess.run(cmd, check=True)
     return out

@@ -21,7 +21,6 @@ p.add_argument("--mode", choices=["reduce", "iterate", "level"], default="reduce
                help="level: the solve's launches at one level (iterations forward, reverse, forward)")
 p.add_argument("--c4", action="store_true", help="channel-quad packed features")
 p.add_argument("--schedule", default=None, help="auto | march | split (channel-quad reduce kernel)")
-p.add_argument("--tail", action="store_true", help="print the launch timeline of a DPFT_TAIL_PROF build")
 p.add_argument("--warm-ms", type=float, default=300.0, help="warm-up time before timing")
 p.add_argument("--from-solve", action="store_true",
                help="start from the poses of one full pyramid solve (the bench's operating point) instead of identity")
@@ -69,26 +68,5 @@ for level in ([a.level] if a.level >= 0 else range(len(solver.calls))):
     torch.cuda.synchronize()
     us = e0.elapsed_time(e1) / (a.reps * per) * 1e3
     gbs = solver.algorithmic_bytes(level) / (us * 1e-6) / 1e9
-    if a.tail:  # DPFT_TAIL_PROF build: ctrl words kCtlTail.. (dpft_ic.hip)
-        import numpy as np
-        CT, NWG, NP = 3264, 768, 16
-        w = solver.ws[:(CT + NWG + 2 * NP + 5) * 4].view(torch.int32).cpu().numpy().astype("int64") & 0xFFFFFFFF
-        nb = int(c.desc.B)
-        g = int(os.environ.get("DPFT_TAIL_GRID", "512"))
-        f = w[CT:CT + g]
-        t0 = f.min()
-        f = (f - t0) / 100.0
-        bs = (w[CT + NWG + 2 * NP:CT + NWG + 2 * NP + 2] - t0) / 100.0
-        pr = (w[CT + NWG:CT + NWG + 2 * nb].reshape(nb, 2) - t0) / 100.0
-        sub = (w[CT + NWG + 2 * NP + 2:CT + NWG + 2 * NP + 5] - t0) / 100.0
-        print("  pair 0 reduce: records loaded %.1f, extrema %.1f, trees %.1f" % tuple(sub))
-        np.save(os.path.join(ROOT, "gpurun_out", f"tail_l{level}_{a.mode}.npy"), f)
-        print("  timeline (us from the first workgroup finish): last workgroup done %.1f, batch-last detected %.1f, "
-              "batch solved %.1f" % (f.max(), bs[0], bs[1]))
-        per = g // nb
-        for b in range(nb):
-            x = f[b * per:(b + 1) * per]
-            print("   pair %d: finish min %.1f  median %.1f  max %.1f | pair-last detected %.1f, pair reduced %.1f"
-                  % (b, x.min(), np.median(x), x.max(), pr[b, 0], pr[b, 1]))
     print(f"{os.path.basename(os.environ.get('DPFT_LIB', 'libdpft_ic.so'))}{' c4' if a.c4 else ''}{' ' + a.schedule if a.schedule else ''} {a.mode} level {level} B={a.batch}x{a.groups}: "
           f"{us:.1f} us/launch, {gbs:.0f} GB/s algorithmic ({gbs / 80:.1f}% of 8 TB/s)", flush=True)
