@@ -5,7 +5,6 @@ pair's row in pair order -- equal to each shard evaluated alone -- and write the
 reference's pkl / CSV (evaluate.py:318-372)."""
 import os
 import pickle
-import socket
 
 import numpy as np
 import torch
@@ -41,9 +40,8 @@ def _solve(d):
 def _worker(rank, world, port, q, paths, out_dir):
     import sys
     sys.path[:0] = paths
-    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     torch.set_num_threads(2)
-    dist.init_process_group("gloo", rank=rank, world_size=world)
+    dist.init_process_group("gloo", init_method=f"file://{port}", rank=rank, world_size=world)
     try:
         rows = E.evaluate_sharded(_load, _solve, len(PAIRS), batch=2)
         if rank == 0:
@@ -51,15 +49,18 @@ def _worker(rank, world, port, q, paths, out_dir):
             from deep_prob_feature_track_amd import metrics
             metrics.write_results({"fr1_desk_keyframe_1": E.rows_to_outputs(rows, names)}, [1], "test",
                                   root=out_dir)
-            q.put(rows.clone())
+            q.put(rows.numpy().copy())
     finally:
         dist.destroy_process_group()
 
 
 def _free_port():
-    with socket.socket() as s:
-        s.bind(("127.0.0.1", 0))
-        return s.getsockname()[1]
+    """A fresh rendezvous file for init_method="file://..." (no TCP port to race for)."""
+    import tempfile
+    fd, path = tempfile.mkstemp(prefix="dpft_gloo_")
+    os.close(fd)
+    os.unlink(path)
+    return path
 
 
 def test_two_rank_sharded_evaluation_writes_reference_outputs(tmp_path):
@@ -72,7 +73,7 @@ def test_two_rank_sharded_evaluation_writes_reference_outputs(tmp_path):
              for r in range(world)]
     for p in procs:
         p.start()
-    rows = q.get(timeout=180)
+    rows = torch.from_numpy(q.get(timeout=180))
     for p in procs:
         p.join(timeout=60)
         assert p.exitcode == 0

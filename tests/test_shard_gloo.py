@@ -8,7 +8,6 @@ batch-global truncated-sigma extrema are per shard, as under the reference's
 nn.DataParallel).
 """
 import os
-import socket
 
 import pytest
 import torch
@@ -54,9 +53,8 @@ def _solve_pairs(pairs):
 def _worker(rank, world, port, q, paths):
     import sys
     sys.path[:0] = paths
-    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     torch.set_num_threads(2)
-    dist.init_process_group("gloo", rank=rank, world_size=world)
+    dist.init_process_group("gloo", init_method=f"file://{port}", rank=rank, world_size=world)
     try:
         b, e = shard.shard_range(len(PAIRS), world, rank)
         R, t = _solve_pairs(PAIRS[b:e])
@@ -67,16 +65,19 @@ def _worker(rank, world, port, q, paths):
         t.zero_()
         work.wait()
         if rank == 0:
-            q.put(out.clone())
-            q.put(out2.clone())
+            q.put(out.numpy().copy())
+            q.put(out2.numpy().copy())
     finally:
         dist.destroy_process_group()
 
 
 def _free_port():
-    with socket.socket() as s:
-        s.bind(("127.0.0.1", 0))
-        return s.getsockname()[1]
+    """A fresh rendezvous file for init_method="file://..." (no TCP port to race for)."""
+    import tempfile
+    fd, path = tempfile.mkstemp(prefix="dpft_gloo_")
+    os.close(fd)
+    os.unlink(path)
+    return path
 
 
 def test_two_rank_gloo_gather_matches_per_shard_solves():
@@ -88,8 +89,8 @@ def test_two_rank_gloo_gather_matches_per_shard_solves():
     procs = [ctx.Process(target=_worker, args=(r, world, port, q, list(sys.path))) for r in range(world)]
     for p in procs:
         p.start()
-    gathered = q.get(timeout=120)
-    gathered_async = q.get(timeout=120)
+    gathered = torch.from_numpy(q.get(timeout=120))
+    gathered_async = torch.from_numpy(q.get(timeout=120))
     for p in procs:
         p.join(timeout=60)
         assert p.exitcode == 0
@@ -102,9 +103,8 @@ def test_two_rank_gloo_gather_matches_per_shard_solves():
 
 
 def _worker_results(rank, world, port, q, n_pairs):
-    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     torch.set_num_threads(1)
-    dist.init_process_group("gloo", rank=rank, world_size=world)
+    dist.init_process_group("gloo", init_method=f"file://{port}", rank=rank, world_size=world)
     try:
         b, e = shard.shard_range(n_pairs, world, rank)
         idx = torch.arange(b, e, dtype=torch.float32).view(-1, 1, 1)
@@ -114,7 +114,7 @@ def _worker_results(rank, world, port, q, n_pairs):
         status = torch.tensor([rank], dtype=torch.int32)
         out = shard.gather_results(R, t, jtj=jtj, status=status, n_pairs=n_pairs)
         if rank == 0:
-            q.put(out.clone())
+            q.put(out.numpy().copy())
     finally:
         dist.destroy_process_group()
 
@@ -130,7 +130,7 @@ def test_two_rank_gather_results_ragged_shards(n_pairs):
     procs = [ctx.Process(target=_worker_results, args=(r, world, port, q, n_pairs)) for r in range(world)]
     for p in procs:
         p.start()
-    out = q.get(timeout=120)
+    out = torch.from_numpy(q.get(timeout=120))
     for p in procs:
         p.join(timeout=60)
         assert p.exitcode == 0
