@@ -48,7 +48,7 @@ def parse():
                    help="> 0: weak scaling instead, this many pairs per GPU per step")
     p.add_argument("--batch", type=int, default=8,
                    help="pairs per independent batch (one reference call: its own batch-global extrema)")
-    p.add_argument("--inflight", type=int, default=2,
+    p.add_argument("--inflight", type=int, default=4,
                    help="consecutive steps of the stream in flight per GPU (one stream, graph, workspace each)")
     p.add_argument("--icp", action="store_true", help="cfg5: with the combine_ICP term (weight 0.01)")
     p.add_argument("--setup-warm-ms", type=float, default=200.0,

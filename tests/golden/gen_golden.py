@@ -46,6 +46,7 @@ OPTIONS = {
     "cfg4_pert05_160x120_c8": dict(remove_tru_sigma=True, combine_icp=False),
     "cfg4_pert10_160x120_c8": dict(remove_tru_sigma=True, combine_icp=False),
     "cfg4_pert20_160x120_c8": dict(remove_tru_sigma=True, combine_icp=False),
+    "cfg4_sweep256_160x120_c8": dict(remove_tru_sigma=True, combine_icp=False),
 }
 
 
@@ -217,7 +218,7 @@ def main(names):
         ref = "f64" if "f64_R" in out else "f32"
         d = np.abs(out["f32_R"][-1] - out[f"{ref}_R"][-1]).max()
         dt = np.abs(out["f32_t"][-1] - out[f"{ref}_t"][-1]).max()
-        print(f"{name}: {time.time() - t0:.1f}s  final t({ref})={out[f'{ref}_t'][-1].tolist()}  "
+        print(f"{name}: {time.time() - t0:.1f}s  final t({ref}) pair 0={out[ref + '_t'][-1][0].tolist()}  "
               f"|f32-f64| R {d:.2e} t {dt:.2e}  invalid(last)={out['f32_invalid'][-1].tolist()}")
 
 

@@ -169,11 +169,12 @@ def so3_exp64(w):
     return np.eye(3) + np.sin(th) * Kx + (1 - np.cos(th)) * Kx @ Kx
 
 
-def make_case(pairs, C, levels, base_down=1, masks=False, icp=False, init=None):
+def make_case(pairs, C, levels, base_down=1, masks=False, icp=False, init=None, flips=None):
     """Build a solver-level case.
 
     pairs: list of (i, j) frame indices (reference i -> target j)
     levels: number of pyramid levels (1 = level 0 only)
+    flips: per-pair flip codes (flip_case), None = none
     Returns dict with per-level arrays and the initial pose.
     """
     B = len(pairs)
@@ -207,6 +208,9 @@ def make_case(pairs, C, levels, base_down=1, masks=False, icp=False, init=None):
         if masks:
             case[f"mask0_{l}"] = any_pool(m0, k)
             case[f"mask1_{l}"] = any_pool(m1, k)
+    if flips is not None:
+        case = flip_case(case, flips)
+        case["flips"] = np.array(flips, np.int32)
     if init is None:
         R = np.tile(np.eye(3, dtype=np.float32)[None], (B, 1, 1))
         t = np.zeros((B, 3), np.float32)
@@ -241,11 +245,12 @@ def sweep_case(B, C=8, levels=4, base_down=4, masks=True):
     """cfg4's batch: B pairs cycled through the 20 ordered pairs of the five frames, each
     round of 20 with its own flip code (80 distinct pairs), object masks = depth below the
     frame's median, identity initial pose."""
-    pairs = [ORDERED_PAIRS[k % len(ORDERED_PAIRS)] for k in range(B)]
-    flips = [(k // len(ORDERED_PAIRS)) % 4 for k in range(B)]
-    case = flip_case(make_case(pairs, C, levels, base_down, masks=masks), flips)
-    case["flips"] = np.array(flips, np.int32)
-    return case
+    return make_case(**sweep_spec(B, C, levels, base_down, masks))
+
+
+def sweep_spec(B, C=8, levels=4, base_down=4, masks=True):
+    return dict(pairs=[ORDERED_PAIRS[k % len(ORDERED_PAIRS)] for k in range(B)], C=C, levels=levels,
+                base_down=base_down, masks=masks, flips=[(k // len(ORDERED_PAIRS)) % 4 for k in range(B)])
 
 
 INPUT_KEYS_PREFIX = ("x0_", "x1_", "s0_", "s1_", "invD0_", "invD1_", "depth0_", "depth1_", "mask0_", "mask1_")
@@ -307,3 +312,5 @@ CASES = {
     "cfg4_pert20_160x120_c8": dict(pairs=CFG4_PAIRS, C=8, levels=4, base_down=4, masks=True,
                                    init=perturbations(4, 0.20, 0.15, 2)),
 }
+# cfg4's full batch: 256 masked pairs (80 distinct: the 20 ordered pairs x 4 flip codes), identity start
+CASES["cfg4_sweep256_160x120_c8"] = sweep_spec(256)

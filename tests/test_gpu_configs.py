@@ -309,54 +309,30 @@ def test_cfg4_start_sets_in_one_grouped_call():
 
 
 def test_cfg4_sweep_b256():
-    """cfg4's batch: 256 masked pairs at 160x120, C = 8 (tests/golden/recipe.py sweep_case).
-    The identity-start solve (the basin's target) against the oracle on the same 256-pair
-    batch: level 0's last iteration restarted from the oracle's pose gives the oracle's
-    invalid counts exactly, and the chained poses lie within the oracle's own envelope under
-    a 1e-7 start change (three jittered oracle runs).  Then a 1-D sweep of perturbed starts
-    around the target (6 axes x 5 offsets up to 0.2 rad / 0.15 m: 30 start sets = 7680
-    solves in grouped calls of 8 start sets): start sets solved in one grouped call equal the
-    same sets solved one call each, and the convergence counts are reported with the number
-    of pairs whose margin is below the pose uncertainty."""
+    """cfg4's batch: 256 masked pairs at 160x120, C = 8 (80 distinct: tests/golden/recipe.py
+    sweep_spec), against the reference's own run of that batch (cfg4_sweep256_160x120_c8):
+    every iteration restarted from the reference's pose gives its invalid counts exactly; the
+    identity-start solve (the basin's target) lies within the reference's 1e-7-jitter
+    envelope.  Then a 1-D sweep of perturbed starts around the target (6 axes x 5 offsets up
+    to 0.2 rad / 0.15 m: 30 start sets = 7680 solves in grouped calls of 8 start sets): start
+    sets solved in one grouped call equal the same sets solved one call each, and the
+    convergence counts are reported with the pairs whose margin is below the pose
+    uncertainty."""
     from deep_prob_feature_track_amd import convergence_basin as cb
-    from deep_prob_feature_track_amd import ic
-    from oracle import ic_oracle as O
     dev = _dev()
-    case = recipe.sweep_case(256)
+    name = "cfg4_sweep256_160x120_c8"
+    _restart_iterations(name, dev, True)
+    case, z = golden_io.load(name)
     B = case["B"]
     K = torch.from_numpy(case["K"]).to(dev)
     lv = _solver_levels(case, dev, True)
     I = torch.eye(3, device=dev).repeat(1, B, 1, 1)
     Rt, tt = cb.solve_from_starts(lv, K, I, torch.zeros(1, B, 3, device=dev))
     Rt, tt = Rt[0], tt[0]
-    # the oracle on the same batch (batch-global extrema over all 256 pairs), plain and jittered
-    lc = golden_io.levels_torch(case, torch.float32)
-    Kc = torch.from_numpy(case["K"])
-    g = torch.Generator().manual_seed(4)
-    runs, trace = [], []
-    with torch.no_grad():
-        for k in range(4):
-            t0 = torch.zeros(B, 3, 1) if k == 0 else (torch.rand(B, 3, 1, generator=g) * 2 - 1) * 1e-7
-            runs.append(O.solve_pyramid(torch.eye(3).repeat(B, 1, 1), t0, lc, Kc, iters=3, remove_tru_sigma=True,
-                                        trace=trace if k == 0 else None))
-    Ro, to = runs[0][0], runs[0][1].view(B, 3)
-    env = torch.stack([torch.maximum((r - Ro).abs().amax((1, 2)), (t.view(B, 3) - to).abs().amax(1))
-                       for r, t in runs[1:]]).amax(0)
-    dev_pose = torch.maximum((Rt.cpu() - Ro).abs().amax((1, 2)), (tt.cpu() - to).abs().amax(1))
-    bound = torch.clamp(2.0 * env, min=SE3_TOL)
-    assert (dev_pose <= bound).all(), f"{int((dev_pose > bound).sum())} pairs outside the oracle's envelope"
-    print(f"cfg4 B=256 identity start vs oracle: {int((dev_pose <= SE3_TOL).sum())} of {B} pairs within 1e-4, "
-          f"max {dev_pose.max().item():.2e} (oracle envelope max {env.max().item():.2e})")
-    # level 0's last iteration from the oracle's own pose: exact invalid counts
-    d = lv[0]
-    it = trace[-2]
-    o = ic.iterate((it["R"].to(dev), it["t"].to(dev).view(B, 3, 1)), d["x0"], d["x1"], d["invD0"], d["invD1"], K,
-                   d["sigma0"], d["sigma1"], first=True, reverse=False, remove_tru_sigma=True,
-                   obj_mask0=d["obj_mask0"], obj_mask1=d["obj_mask1"])
-    assert np.array_equal(o[4].cpu().numpy(), trace[-1]["invalid"].numpy())
-    jr = trace[-1]["JtJ"].numpy()
-    assert np.abs(o[2].cpu().numpy() - jr).max() / np.abs(jr).max() < 1e-5
-    # the sweep
+    dev_pose, env = _assert_within_reference_envelope(Rt, tt, z, what=name)
+    print(f"cfg4 B=256 identity start vs reference: {int((dev_pose <= SE3_TOL).sum())} of {B} pairs within 1e-4, "
+          f"max {dev_pose.max():.2e} (reference envelope max {env.max():.2e})")
+    bound = np.maximum(SE3_TOL, 2.0 * env)
     rot = np.linspace(-0.2, 0.2, 5)
     trs = np.linspace(-0.15, 0.15, 5)
     Rs, ts = cb.perturbed_starts(Rt, tt, rot, trs)
@@ -364,11 +340,10 @@ def test_cfg4_sweep_b256():
     Rf, tf = cb.solve_from_starts(lv, K, Rs, ts)
     for p in (0, 13, 29):  # grouped = one call per start set (summation grouping only)
         Ra, ta = cb.solve_from_starts(lv, K, Rs[p:p + 1], ts[p:p + 1])
-        close = torch.maximum((Rf[p] - Ra[0]).abs().amax((1, 2)), (tf[p] - ta[0]).abs().amax(1))
-        assert (close.cpu() <= bound).all(), f"start set {p}: grouped vs alone {close.max().item():.2e}"
+        close = torch.maximum((Rf[p] - Ra[0]).abs().amax((1, 2)), (tf[p] - ta[0]).abs().amax(1)).cpu().numpy()
+        assert (close <= bound).all(), f"start set {p}: grouped vs alone {close.max():.2e}"
     counts, m = cb.basin_counts(Rf, tf, Rt, tt, rot_thresh=0.01, trans_thresh=0.01)
-    unc = bound.numpy()[None]
-    near = (np.abs(m["rot_margin"]) < unc) | (np.abs(m["trans_margin"]) < unc)
+    near = (np.abs(m["rot_margin"]) < bound[None]) | (np.abs(m["trans_margin"]) < bound[None])
     assert all(counts[a * 5 + 2] >= B - near[a * 5 + 2].sum() for a in range(6))  # zero-offset starts
     print("cfg4 sweep counts (6 axes x 5 offsets):", counts.reshape(6, 5).tolist(),
           "undecided (margin < uncertainty):", near.sum(1).reshape(6, 5).tolist())
