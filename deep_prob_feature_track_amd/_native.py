@@ -24,6 +24,7 @@ EXTREMA_READY = 0x10000
 GROUP_SHIFT = 20          # DPFT_GROUP(n) = n << 20: n pairs per independent batch (bits 20-31)
 GROUP_MAX_BATCHES = 32
 STATUS_NONFINITE = 0x1
+CTRL_BYTES = 20480        # the workspace's control area (counters): zero before first use (kCtrlBytes)
 ABI_VERSION = 2
 
 

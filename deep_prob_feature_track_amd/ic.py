@@ -21,6 +21,12 @@ _ws_cache = {}
 _ws_retired = []
 
 
+def _eager_only(fn):
+    """ctypes calls are opaque to dynamo: under torch.compile these run eagerly (a graph
+    break) -- the drop-in's traced path uses the dpft:: ops of torch_ops.py instead."""
+    return torch.compiler.disable(fn, recursive=True)
+
+
 def _workspace(device, nbytes):
     """The per-(device, stream) workspace of the one-call entry points: one per stream
     because concurrent launches must not share completion counters (dpft_ic.h).  A
@@ -60,6 +66,7 @@ def _sigma_planes(sigma, B, C, H, W):
     return sigma.contiguous(), C
 
 
+@_eager_only
 def pack_features(x):
     """Feature map [B,C,H,W] -> channel-quad layout [B,C/4,H,W,4] (dpft_pack_features).
 
@@ -105,6 +112,7 @@ def _bn_coeffs(bn, device):
     return chan
 
 
+@_eager_only
 def bn_elu_(x, bn):
     """In place x = ELU(bn(x)) for an eval-mode BatchNorm2d with running statistics
     (the reference's convLayer epilogue, submodules.py:25-39) in one pass
@@ -172,7 +180,7 @@ class LevelCall:
     def __init__(self, x0, x1, invD0, invD1, K, sigma0, sigma1, iters=3, remove_tru_sigma=False,
                  obj_mask0=None, obj_mask1=None, depth0=None, depth1=None, combine_icp=False,
                  icp_weight=0.01, status=None, no_uncertainty=False, pack=False, schedule=None, weights=None,
-                 group=None):
+                 group=None, private_workspace=False):
         if not x0.is_cuda:
             raise RuntimeError("the HIP solver needs device tensors (got CPU); there is no CPU fallback")
         for name, t in (("x0", x0), ("x1", x1), ("invD0", invD0), ("invD1", invD1), ("K", K)):
@@ -244,7 +252,13 @@ class LevelCall:
         if nbytes == 0:
             N.check(-1, "dpft_workspace_size")
         self.ws_bytes = nbytes
-        self.ws = _workspace(self.device, nbytes)
+        # private_workspace: a zero-filled buffer of this call's own (the dpft:: ops: a
+        # buffer cached across calls would outlive a torch.compile CUDA-graph capture)
+        if private_workspace:  # only the control words (completion counters) must start at zero
+            self.ws = torch.empty(nbytes, dtype=torch.uint8, device=self.device)
+            self.ws[:min(nbytes, N.CTRL_BYTES)].zero_()
+        else:
+            self.ws = _workspace(self.device, nbytes)
 
     def pose_buffers(self, pose):
         R, t = pose
@@ -253,12 +267,14 @@ class LevelCall:
         return R, t
 
 
+@_eager_only
 def check_status(status):
     """Mirror of `assert check_nan(...) == 0` (algorithms.py:886, 1988): one host read."""
     if int(status.item()) & N.STATUS_NONFINITE:
         raise AssertionError("non-finite Jacobian / residual in the IC solver (reference: check_nan assert)")
 
 
+@_eager_only
 def solve_level(pose, x0, x1, invD0, invD1, K, sigma0, sigma1, iters=3, return_jtj=False, check=True, **kw):
     """`iters` Gauss-Newton steps at one level; returns (R [B,3,3], t [B,3,1][, JtJ [B,6,6]]).
     pack=True (keyword) packs eligible NCHW features first (pays off from 2 iterations)."""
@@ -274,6 +290,7 @@ def solve_level(pose, x0, x1, invD0, invD1, K, sigma0, sigma1, iters=3, return_j
     return out + (jtj,) if return_jtj else out
 
 
+@_eager_only
 def iterate(pose, x0, x1, invD0, invD1, K, sigma0, sigma1, first=True, reverse=False, update=True, **kw):
     """One iteration; returns (R, t [B,3,1], JtJ [B,6,6], JtR [B,6], invalid [B]) -- test / trace API.
     reverse=True: the marching order of the solve's odd iterations (DPFT_ITER_REVERSE).
@@ -291,6 +308,7 @@ def iterate(pose, x0, x1, invD0, invD1, K, sigma0, sigma1, first=True, reverse=F
     return R, t.view(c.B, 3, 1), jtj, jtr, inv
 
 
+@_eager_only
 def iterate_poses(R, t, x0, x1, invD0, invD1, K, sigma0, sigma1, **kw):
     """J^T J and J^T R at S poses per pair, no update: R [S,B,3,3], t [S,B,3(,1)] ->
     (JtJ [S,B,6,6], JtR [S,B,6]).  One validated LevelCall (workspace, pointers) for all
@@ -319,6 +337,7 @@ def _dev_f32(name, t):
     return t.contiguous()
 
 
+@_eager_only
 def feature_gradient(f):
     """Unit-normalised Sobel (feature_gradient, algorithms.py:1844-1865): f [B,C,H,W] ->
     [B,C,2,H,W], (x, y) stacked on dim 2 as precompute_jacobian_components stacks them."""
@@ -329,6 +348,7 @@ def feature_gradient(f):
     return g
 
 
+@_eager_only
 def warp_jacobian(invD0, K, px, py):
     """compute_jacobian_warping at the origin (algorithms.py:1884-1917) -> Jx, Jy [B,HW,6]."""
     invD0 = _dev_f32("invD0", invD0)
@@ -343,6 +363,7 @@ def warp_jacobian(invD0, K, px, py):
     return Jx, Jy
 
 
+@_eager_only
 def inverse_jacobian(res, sigma, sigma0, grad_f0, grad_sigma0, Jx, Jy):
     """compose_inverse_jacobians' J (algorithms.py:867-887): [B,C,HW,6], not masked.
     sigma0 / grad_sigma0 may carry one channel or C (a channel broadcast is read once)."""
@@ -361,6 +382,7 @@ def inverse_jacobian(res, sigma, sigma0, grad_f0, grad_sigma0, Jx, Jy):
     return J
 
 
+@_eager_only
 def normal_equations(J, r=None):
     """compute_jtj / compute_jtr (algorithms.py:812-834): J [B,...,6] (rows = every
     channel and pixel), r [B,...] -> (JtJ [B,6,6], JtR [B,6,1] or None); fixed-order fp64."""
@@ -381,6 +403,7 @@ def normal_equations(J, r=None):
     return jtj, jtr
 
 
+@_eager_only
 def damped_update(JtJ, JtR, diag_add, pose):
     """S damped inverse-compositional updates per pair in one launch (dpft_ic_damped_update):
     JtJ [B,6,6], JtR [B,6], diag_add [S,B,6] or None (S = 1), pose ([B,3,3], [B,3(,1)])
@@ -403,6 +426,7 @@ def damped_update(JtJ, JtR, diag_add, pose):
     return R_out, t_out
 
 
+@_eager_only
 def residual_map(pose, x0, x1, invD0, invD1, K, **kw):
     """IC tracker residuals at `pose` (compute_warped_residual, algorithms.py:1919-1957):
     (r [B,C,H,W] with 1e-3 on occluded / masked pixels, occ [B,1,H,W] bool)."""
@@ -418,6 +442,7 @@ def residual_map(pose, x0, x1, invD0, invD1, K, **kw):
     return out, occ.bool()
 
 
+@_eager_only
 def residual_level(pose, x0, x1, invD0, invD1, K, sigma0, sigma1, **kw):
     """forward_residuals: per-pair average loss [B] at a fixed pose."""
     c = LevelCall(x0, x1, invD0, invD1, K, sigma0, sigma1, iters=1, **kw)
@@ -429,6 +454,7 @@ def residual_level(pose, x0, x1, invD0, invD1, K, sigma0, sigma1, **kw):
     return loss
 
 
+@_eager_only
 def residual_poses(R, t, x0, x1, invD0, invD1, K, sigma0, sigma1, **kw):
     """forward_residuals for P poses per pair in one launch: R [P,B,3,3], t [P,B,3(,1)] -> loss [P,B].
 
@@ -452,7 +478,8 @@ def residual_poses(R, t, x0, x1, invD0, invD1, K, sigma0, sigma1, **kw):
     return loss
 
 
-def preprocess_depth(depth, levels=4, depth_pyramid=False):
+@_eager_only
+def preprocess_depth(depth, levels=4, depth_pyramid=False, workspace=None):
     """LeastSquareTracking._preprocess on the device: invD = clamp(1/depth, 0, 10) with the
     batch-global min then max zeroed, and MaxPool(2^l) pyramids of invD (and of depth).
     depth [B,1,H,W] fp32 on a HIP device -> ([invD_l], [depth_l] or None)."""
@@ -468,12 +495,13 @@ def preprocess_depth(depth, levels=4, depth_pyramid=False):
     darr = (ctypes.c_void_p * levels)(*[t.data_ptr() for t in dep]) if dep else None
     L = N.lib()
     nbytes = L.dpft_preprocess_workspace_size()
-    ws = _workspace(d.device, nbytes)
+    ws = workspace if workspace is not None else _workspace(d.device, nbytes)
     rc = L.dpft_preprocess_depth(_ptr(d), B, H, W, levels, arr, darr, _ptr(ws), nbytes, _stream(d.device))
     N.check(rc, "dpft_preprocess_depth")
     return inv, dep
 
 
+@_eager_only
 def debug_pixels(pose, x0, x1, invD0, invD1, K, sigma0, sigma1, **kw):
     """Per-pixel dump [B,5,H,W] (u, v, sigma_r ch0, sigma0 ch0, occlusion|mask invalid) -- tests only."""
     c = LevelCall(x0, x1, invD0, invD1, K, sigma0, sigma1, iters=1, **kw)

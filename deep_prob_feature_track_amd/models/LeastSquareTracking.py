@@ -27,6 +27,7 @@ from .algorithms import (DeepRobustEstimator, DirectSolverNet, FeaturePyramid, I
                          SFMPoseNet, TrustRegionBase, TrustRegionInverseWUncertainty)
 from .submodules import color_normalize
 from .. import ic
+from .. import torch_ops  # noqa: F401  (registers the dpft:: ops torch.compile traces)
 
 # options attributes the reference constructor reads, with config.py's defaults
 DEFAULT_OPTIONS = dict(vis_feat=False, train_uncer_prop=False, combine_ICP=False, feature_extract='average',
@@ -157,7 +158,10 @@ class LeastSquareTracking(nn.Module):
         # U_IC: the four levels share one status word, read once after the finest level
         # (the reference asserts per iteration; either way a non-finite Jacobian or
         # residual raises AssertionError out of forward and no pose is returned)
-        status = torch.zeros(1, dtype=torch.int32, device=x0[0].device) if self.track_type != 'IC' else None
+        compiling = torch.compiler.is_compiling()
+        status = None
+        if self.track_type != 'IC' and not compiling:
+            status = torch.zeros(1, dtype=torch.int32, device=x0[0].device)
         try:
             for l in (3, 2, 1, 0):
                 tr = getattr(self, f'tr_update{l}')
@@ -166,6 +170,10 @@ class LeastSquareTracking(nn.Module):
                     out = tr(pose, x0[l], x1[l], inv_d0[l], inv_d1[l], Kl, wPrior, vis_res=False,
                              obj_mask0=m0[l], obj_mask1=m1[l])
                     wPrior = out[1]
+                elif compiling:  # traced: dpft::ic_solve_level ops, the levels' status words OR-ed
+                    out = tr.solve(pose, x0[l], x1[l], inv_d0[l], inv_d1[l], Kl, sigma0[l], sigma1[l], dpt0[l],
+                                   dpt1[l], m0[l], m1[l])
+                    status = out[3] if status is None else torch.bitwise_or(status, out[3])
                 else:
                     tr._deferred_status = status
                     out = tr(pose, x0[l], x1[l], inv_d0[l], inv_d1[l], Kl, sigma0=sigma0[l], sigma1=sigma1[l],
@@ -173,9 +181,14 @@ class LeastSquareTracking(nn.Module):
                              obj_mask1=m1[l])
                 pose = out[0]
         finally:
-            for l in (3, 2, 1, 0):
-                getattr(self, f'tr_update{l}')._deferred_status = None
+            if not compiling:
+                for l in (3, 2, 1, 0):
+                    getattr(self, f'tr_update{l}')._deferred_status = None
         self.last_status = status
+        if compiling:
+            # traced (torch.compile): no host read inside the graph -- the caller checks
+            # `model.last_status` (ic.check_status), as after a HIP-graph replay
+            return pose
         # under HIP-graph capture the host read is deferred to the caller (check
         # `model.last_status` after a replay, e.g. ic.check_status): forward is then
         # capturable whole -- encoder, pyramids and the four levels in one graph
@@ -256,8 +269,15 @@ class LeastSquareTracking(nn.Module):
     def _preprocess(self, img0, img1, depth0, depth1, poseI=None, obj_mask0=None, obj_mask1=None):
         """LeastSquareTracking.py:653-699."""
         if depth0.is_cuda:  # fused device pre-pass (dpft_preprocess_depth), bit-identical to the torch ops
-            inv_d0, dp0 = ic.preprocess_depth(depth0, len(self.scales), depth_pyramid=self.combine_icp)
-            inv_d1, dp1 = ic.preprocess_depth(depth1, len(self.scales), depth_pyramid=self.combine_icp)
+            L = len(self.scales)
+            if torch.compiler.is_compiling():  # traced: the dpft::preprocess_depth op
+                o0 = torch.ops.dpft.preprocess_depth(depth0, L, bool(self.combine_icp))
+                o1 = torch.ops.dpft.preprocess_depth(depth1, L, bool(self.combine_icp))
+                inv_d0, inv_d1 = o0[:L], o1[:L]
+                dp0, dp1 = (o0[L:], o1[L:]) if self.combine_icp else (None, None)
+            else:
+                inv_d0, dp0 = ic.preprocess_depth(depth0, L, depth_pyramid=self.combine_icp)
+                inv_d1, dp1 = ic.preprocess_depth(depth1, L, depth_pyramid=self.combine_icp)
             invD0, invD1 = inv_d0[0], inv_d1[0]
         else:
             invD0 = self._inverse_depth(depth0)

@@ -21,6 +21,7 @@ import torch.nn as nn
 import torch.nn.functional as func
 
 from .. import ic
+from .. import torch_ops  # noqa: F401  (registers the dpft:: ops torch.compile traces)
 from . import geometry
 from .submodules import convLayer as conv
 from .submodules import convLayer1d as conv1d
@@ -535,20 +536,39 @@ class TrustRegionInverseWUncertainty(nn.Module):
 
     def forward(self, pose10, x0, x1, invD0, invD1, K, sigma0, sigma1, wPrior=None,
                 depth0=None, depth1=None, vis_res=True, obj_mask0=None, obj_mask1=None):
+        out = self.solve(pose10, x0, x1, invD0, invD1, K, sigma0, sigma1, depth0, depth1, obj_mask0, obj_mask1)
+        if self._deferred_status is None:
+            ic.check_status(out[3])
+        return out[:3] if self.uncer_prop else out[:2]
+
+    def solve(self, pose10, x0, x1, invD0, invD1, K, sigma0, sigma1, depth0=None, depth1=None, obj_mask0=None,
+              obj_mask1=None):
+        """-> (pose [R, t], weights, JtWJ or None, status [1] int32 device word): forward
+        without the host check.  Traced by torch.compile it is one dpft::ic_solve_level op
+        (torch_ops.py); eager, the same library call through ctypes."""
         assert sigma0 is not None and sigma1 is not None
         self._check_path(x0)
         B, C, H, W = x0.shape
         kw = self._common(x0, depth0, depth1, obj_mask0, obj_mask1)
-        st = self._deferred_status
         with torch.no_grad():
-            out = ic.solve_level(pose10, x0, x1, invD0, invD1, K, sigma0, sigma1, iters=self.max_iterations,
-                                 return_jtj=self.uncer_prop, check=st is None, status=st, **kw)
+            if torch.compiler.is_compiling():
+                R, t, jtj, status = torch.ops.dpft.ic_solve_level(
+                    pose10[0], pose10[1], x0, x1, invD0, invD1, K, sigma0, sigma1, kw.get("depth0"),
+                    kw.get("depth1"), obj_mask0, obj_mask1, self.max_iterations, bool(self.remove_tru_sigma),
+                    bool(self.combine_icp), float(kw.get("icp_weight", 0.01)), False, bool(self.uncer_prop))
+                out = (R, t, jtj if self.uncer_prop else None)
+            else:
+                status = self._deferred_status
+                if status is None:
+                    status = torch.zeros(1, dtype=torch.int32, device=x0.device)
+                out = ic.solve_level(pose10, x0, x1, invD0, invD1, K, sigma0, sigma1, iters=self.max_iterations,
+                                     return_jtj=self.uncer_prop, check=False, status=status, **kw)
         pose = [out[0], out[1]]
         if self.combine_icp:
             weights = torch.full((1, 1, 1, 1), self._icp_scale(), dtype=x0.dtype, device=x0.device).expand(B, 1, H, W)
         else:
             weights = torch.ones((1, 1, 1, 1), dtype=x0.dtype, device=x0.device).expand(B, C, H, W)
-        return (pose, weights, out[2]) if self.uncer_prop else (pose, weights)
+        return pose, weights, (out[2] if self.uncer_prop else None), status
 
     # ---- the reference solver's Jacobian API (algorithms.py:812-887), materialised by HIP
     # kernels for callers that inspect J; forward never builds J (it stays in registers)
@@ -599,4 +619,9 @@ class TrustRegionInverseWUncertainty(nn.Module):
         self._check_path(x0)
         kw = self._common(x0, depth0, depth1, obj_mask0, obj_mask1)
         with torch.no_grad():
+            if torch.compiler.is_compiling():
+                return torch.ops.dpft.ic_residual_level(
+                    pose10[0], pose10[1], x0, x1, invD0, invD1, K, sigma0, sigma1, kw.get("depth0"), kw.get("depth1"),
+                    obj_mask0, obj_mask1, bool(self.remove_tru_sigma), bool(self.combine_icp),
+                    float(kw.get("icp_weight", 0.01)), False)
             return ic.residual_level(pose10, x0, x1, invD0, invD1, K, sigma0, sigma1, **kw)

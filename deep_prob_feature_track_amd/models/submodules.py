@@ -11,6 +11,7 @@ import torch.nn as nn
 from torch.nn import init
 
 from .. import ic
+from .. import torch_ops  # noqa: F401  (registers the dpft:: ops torch.compile traces)
 
 _RGB_MEAN = (0.4914, 0.4822, 0.4465)
 _RGB_STD = (0.2023, 0.1994, 0.2010)
@@ -47,7 +48,11 @@ class ConvBlock(nn.Sequential):
         if len(self) == 3 and isinstance(self[1], nn.BatchNorm2d) and isinstance(self[2], nn.ELU) \
                 and self[2].alpha == 1.0 and not self.training and x.is_cuda and not torch.is_grad_enabled():
             y = self[0](x)
-            if ic.bn_elu_(y, self[1]):
+            if torch.compiler.is_compiling():  # traced: the dpft::bn_elu_ op (torch_ops.py)
+                if torch_ops.bn_elu_applies(y, self[1]):
+                    torch.ops.dpft.bn_elu_(y, torch_ops.bn_coeffs(self[1]))
+                    return y
+            elif ic.bn_elu_(y, self[1]):
                 return y
             return self[2](self[1](y))
         return super().forward(x)

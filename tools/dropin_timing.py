@@ -24,6 +24,8 @@ ap.add_argument("--config", default="uic", choices=["uic", "uic8", "deepic"],
                 help="uic: ConvRGBD2 + laplacian U_IC tracker, C=32 (uic8: C=8); deepic: RGB features, IC tracker, "
                      "MultiScale2w M-estimator, Direct-ResVol")
 ap.add_argument("--down", type=int, default=1, help="image subsampling (1: 640x480)")
+ap.add_argument("--compile", default="", help="also time torch.compile(model, backend=...) (comma list, e.g. "
+                                               "aot_eager,cudagraphs)")
 a = ap.parse_args()
 dev = torch.device("cuda:0")
 if os.environ.get("DPFT_DROPIN_BENCHMARK"):  # MIOpen algorithm search for the encoder convs
@@ -71,6 +73,24 @@ if os.environ.get("DPFT_DROPIN_GRAPH"):  # the whole forward captured into one H
             m.forward(img0, img1, d0, d1, K)
     gr = timed(graph.replay)
     print(f"forward as one HIP graph replay: {gr:.2f} ms per call (eager {full:.2f} ms)", flush=True)
+if a.compile:  # torch.compile over the dpft:: ops (torch_ops.py): one traced graph, no code generation
+    m.requires_grad_(False)  # an inference module: no autograd state for the graph backends to track
+    for backend in a.compile.split(","):
+        torch._dynamo.reset()
+        mc = torch.compile(m, backend=backend)
+
+        def call():
+            if backend == "cudagraphs":
+                torch.compiler.cudagraph_mark_step_begin()
+            return mc(img0, img1, d0, d1, K)
+        with torch.no_grad():
+            Re, te = m.forward(img0, img1, d0, d1, K)
+            for _ in range(3):
+                Rc, tc = call()
+            diff = max((Re - Rc).abs().max().item(), (te - tc).abs().max().item())
+        cm = timed(call)
+        print(f"torch.compile(backend={backend}): {cm:.2f} ms per call (eager {full:.2f} ms); "
+              f"max |pose - eager pose| {diff:.1e}", flush=True)
 pre = timed(lambda: m._preprocess(img0, img1, d0, d1))
 H, W = img0.shape[2:]
 print(f"drop-in forward ({a.config}) B={B} {W}x{H}: {full:.2f} ms per call; _preprocess {pre:.2f} ms; "
