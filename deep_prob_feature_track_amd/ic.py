@@ -17,6 +17,8 @@ import torch
 
 from . import _native as N
 
+MAX_PAIRS_PER_CALL = 2048  # pairs per library call (kMaxPairs: one completion counter each)
+
 _ws_cache = {}
 _ws_retired = []
 

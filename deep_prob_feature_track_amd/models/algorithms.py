@@ -462,7 +462,11 @@ class TrustRegionBase(nn.Module):
         resvol = getattr(self.directSolver, 'type', 0) == DirectSolverNet.SOLVER_RESIDUAL_VOLUME
         with torch.no_grad():
             w, _, _ = self._weights(pose, x0, x1, invD0, invD1, K, wPrior, obj_mask0, obj_mask1)
-            rep = self.directSolver.replicate((x0, x1, invD0, invD1, K), w, obj_mask1) if resvol else None
+            # one launch over (trial, pair) rows while they fit a call (ic.MAX_PAIRS_PER_CALL);
+            # larger batches take iterate_poses (one no-update call per trial)
+            rep = None
+            if resvol and self.directSolver.samples * B <= ic.MAX_PAIRS_PER_CALL:
+                rep = self.directSolver.replicate((x0, x1, invD0, invD1, K), w, obj_mask1)
             for it in range(self.max_iterations):
                 m0 = obj_mask0 if it == 0 else None
                 if resvol:

@@ -202,3 +202,22 @@ def test_forward_captured_in_a_hip_graph():
         torch.cuda.synchronize()
         R_s, t_s = m(T["img1"], T["img0"], T["depth1"], T["depth0"], T["K"])
         assert (R_g - R_s).abs().max().item() < 1e-5 and (t_g - t_s).abs().max().item() < 1e-5
+
+
+@pytest.mark.gpu
+def test_resvol_batch_beyond_one_call_of_trials():
+    """'Direct-ResVol' with B = 208 pairs: the ten trials x 208 pairs exceed one library call
+    (2048 pairs), so the trials run one no-update call each (ic.iterate_poses) instead of the
+    replicated launch -- same poses: every replica of the fixture's pairs lands on the
+    reference's (B > 204 used to fail with DPFT_E_INVALID)."""
+    name = "rgb_ic_mest2w_resvol"
+    m, T = _loaded(name, "cuda")
+    z = np.load(os.path.join(HERE, f"model_{name}.npz"), allow_pickle=False)
+    b = T["img0"].shape[0]
+    reps = -(-208 // b)
+    big = {k: v.repeat(reps, *([1] * (v.dim() - 1))) for k, v in T.items()}
+    with torch.no_grad():
+        R, t = m(big["img0"], big["img1"], big["depth0"], big["depth1"], big["K"])
+    assert R.shape[0] == b * reps >= 208
+    assert np.abs(R.cpu().numpy() - np.tile(z["R"], (reps, 1, 1))).max() < 1e-4
+    assert np.abs(t.cpu().numpy().reshape(-1, 3) - np.tile(z["t"].reshape(b, 3), (reps, 1))).max() < 1e-4

@@ -1,0 +1,115 @@
+// Micro-benchmark: the marching kernel's HBM access pattern for channel-group layouts of
+// G = 4 (the shipped channel quads), 8, 16, 32 (NHWC) floats per pixel and group.
+// One wave marches one band of rows of one 62-column strip (lanes = columns 62 s - 1 ..
+// 62 s + 62); per row and channel group it loads the next f0 row of its column and the
+// leading f1 tap pair (two horizontally adjacent pixels of the row below the warped
+// position -- the tap cache of the real kernel supplies the other pair).  Every layout
+// issues the same 16-byte loads per pixel row (C / 4 f0 + C / 2 f1); only the addresses
+// differ.  80 KB of LDS per workgroup pins the real kernel's 2 workgroups per CU.
+//   hipcc --offload-arch=gfx950 -O3 -o /tmp/mbl tools/mb_layout.hip && /tmp/mbl
+#include <hip/hip_runtime.h>
+
+#include <cstdio>
+#include <cstdlib>
+
+#define CHECK(x)                                                           \
+  do {                                                                     \
+    hipError_t e = (x);                                                    \
+    if (e != hipSuccess) {                                                 \
+      printf("%s:%d %s\n", __FILE__, __LINE__, hipGetErrorString(e));     \
+      exit(1);                                                             \
+    }                                                                      \
+  } while (0)
+
+constexpr int W = 640, H = 480, C = 32, NP = 64, STRIPS = 11, BANDS = 3;
+typedef int v4i __attribute__((ext_vector_type(4)));
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+__device__ f32x4 bload(v4i, int, int, int) __asm("llvm.amdgcn.raw.buffer.load.v4f32");
+
+__device__ inline v4i rsrc(const void* p, uint32_t bytes) {
+  const uint64_t a = (uint64_t)p;
+  v4i r;
+  r.x = (int)(a & 0xffffffffu);
+  r.y = (int)(a >> 32);
+  r.z = (int)bytes;
+  r.w = 0x00020000;
+  return r;
+}
+
+// layout G: frame [C/G][H][W][G] floats; the 16-byte chunk k (0 .. C/4-1) of pixel (x, y)
+// lies at ((k / (G/4)) * H * W + y * W + x) * G * 4 + (k % (G/4)) * 16 bytes
+template <int G>
+__global__ __launch_bounds__(256) void march(const float* f0, const float* f1, float* out, float rot, float shift) {
+  __shared__ float pin[80 * 1024 / 4];  // the real kernel's LDS footprint: 2 workgroups per CU
+  constexpr int NG = C / G, PER = G / 4;
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int task = blockIdx.x * 4 + wave;  // (pair, strip, band), band-major within a pair
+  const int b = task / (STRIPS * BANDS), rest = task % (STRIPS * BANDS);
+  if (b >= NP) return;
+  const int band = rest / STRIPS, s = rest % STRIPS;
+  const int xs = s * 62 - 1 + lane, xc = min(max(xs, 0), W - 1);
+  const int y0 = band * H / BANDS, y1 = (band + 1) * H / BANDS;
+  const uint32_t frame = (uint32_t)H * W * C * 4;
+  const v4i r0 = rsrc(f0 + (size_t)b * H * W * C, frame), r1 = rsrc(f1 + (size_t)b * H * W * C, frame);
+  f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+  for (int y = y0; y < y1; ++y) {
+    const int yn = min(y + 1, H - 1);
+    const float u = xc + rot * (y - H / 2) + shift, v = y - rot * (xc - W / 2) + shift;
+    const int tx = min(max((int)floorf(u), 0), W - 2), ty = min(max((int)floorf(v) + 1, 0), H - 1);
+    // all 24 loads of the row in flight in every layout (equal memory-level parallelism);
+    // a group's chunks are issued back to back (same cache lines)
+    f32x4 l[3 * C / 4];
+#pragma unroll
+    for (int g = 0; g < NG; ++g) {
+      const int gp = g * H * W;
+#pragma unroll
+      for (int k = 0; k < PER; ++k) {
+        l[3 * (g * PER + k)] = bload(r0, ((gp + yn * W + xc) * G) * 4 + 16 * k, 0, 2);
+        l[3 * (g * PER + k) + 1] = bload(r1, ((gp + ty * W + tx) * G) * 4 + 16 * k, 0, 0);
+        l[3 * (g * PER + k) + 2] = bload(r1, ((gp + ty * W + tx + 1) * G) * 4 + 16 * k, 0, 0);
+      }
+    }
+    asm volatile("" ::: "memory");
+#pragma unroll
+    for (int k = 0; k < 3 * C / 4; ++k) acc += l[k];
+  }
+  pin[threadIdx.x] = acc.x;
+  if (acc.x + acc.y + acc.z + acc.w == 12345.f) out[0] = pin[(threadIdx.x + 1) & 255];
+}
+
+template <int G>
+void run(const float* f0, const float* f1, float* out) {
+  const int grid = (NP * STRIPS * BANDS + 3) / 4;
+  hipEvent_t e0, e1;
+  CHECK(hipEventCreate(&e0));
+  CHECK(hipEventCreate(&e1));
+  for (int i = 0; i < 5; ++i) march<G><<<grid, 256>>>(f0, f1, out, 0.05f, 0.3f);
+  CHECK(hipEventRecord(e0));
+  const int reps = 20;
+  for (int i = 0; i < reps; ++i) march<G><<<grid, 256>>>(f0, f1, out, 0.05f, 0.3f);
+  CHECK(hipEventRecord(e1));
+  CHECK(hipEventSynchronize(e1));
+  float ms;
+  CHECK(hipEventElapsedTime(&ms, e0, e1));
+  const double us = ms * 1e3 / reps;
+  const double alg = 2.0 * NP * H * W * C * 4;  // f0 + f1 once each
+  printf("G=%2d (%s): %7.1f us per launch, %6.0f GB/s algorithmic (f0 + f1)\n", G,
+         G == 4 ? "channel quads" : G == 32 ? "NHWC" : "channel groups", us, alg / (us * 1e-6) / 1e9);
+}
+
+int main() {
+  const size_t n = (size_t)NP * C * W * H;
+  float *f0, *f1, *out;
+  CHECK(hipMalloc(&f0, n * 4));
+  CHECK(hipMalloc(&f1, n * 4));
+  CHECK(hipMalloc(&out, 4));
+  CHECK(hipMemset(f0, 0, n * 4));
+  CHECK(hipMemset(f1, 0, n * 4));
+  for (int rep = 0; rep < 2; ++rep) {
+    run<4>(f0, f1, out);
+    run<8>(f0, f1, out);
+    run<16>(f0, f1, out);
+    run<32>(f0, f1, out);
+  }
+  return 0;
+}
