@@ -1348,7 +1348,30 @@ __global__ __launch_bounds__(kThreads, 1) void ic_reduce_kernel(IterParams p) {
     const int hTf = min(H, (U * (64 + hsk)) / hwt), hTu = min(H, (U * (64 - hsk)) / hwt);
     const int hnf = min(hh, S_), hLf = H - hTf, hLu = H - hTu;
     const bool hpool = hyb && band >= S_;
-    if (hyb && !hpool) {
+    // grid + pool split (2 S < nw, no waste-free grid: the 64-pair launch's 32 waves over 11
+    // strips): Kg = ceil(nw / S) row bands with common cuts give Kg S >= nw segments; wave w
+    // marches segment w (band w / S, strip w % S) and the Eg = Kg S - nw segments left over
+    // (the last band's last strips) are split strip-major over all nw waves, marched after
+    // each wave's own segment.  So Eg / (Kg S) of the units (1 in 33 at 64 pairs) run without
+    // their horizontal neighbours in lockstep, against all of them on the strip-major split.
+    // Band cuts weight each band by its segments' waves (64 + skew in the first half of the
+    // pair's waves, 64 - skew in the second, 64 for a left-over segment).
+    const int Kg = (nw + S_ - 1) / S_, Eg = Kg * S_ - nw;
+    const bool gpool = !grid && !hyb && Kg >= 3;
+    auto gp_w = [&](int n) {  // weight of segments 0 .. n - 1
+      return (long)(64 + hsk) * min(n, hh) + (long)(64 - hsk) * min(max(n - hh, 0), nw - hh) + 64L * max(n - nw, 0);
+    };
+    auto gp_cut = [&](int k) { return (int)(((long)H * gp_w(k * S_)) / gp_w(Kg * S_)); };
+    const int gk = band / S_, gs = band - gk * S_;
+    const int gr0 = gpool ? gp_cut(gk) : 0, gr1 = gpool ? gp_cut(gk + 1) : 0;  // main rows [gr0, gr1)
+    const int gL0 = gpool ? gp_cut(Kg - 1) : 0, gHL = H - gL0;                 // the last band's rows
+    const int gPU = Eg * gHL, gpb = gpool ? (int)(((long)gPU * band) / nw) : 0;
+    const int gpe = gpool ? (int)(((long)gPU * (band + 1)) / nw) : 0;  // pool units [gpb, gpe)
+    if (gpool) {
+      ubeg = 0;
+      uend = (gr1 - gr0) + (gpe - gpb);
+      vband = gk;
+    } else if (hyb && !hpool) {
       ubeg = band * H;
       uend = band * H + (band < hh ? hTf : hTu);
       vband = 0;
@@ -1385,6 +1408,22 @@ __global__ __launch_bounds__(kThreads, 1) void ic_reduce_kernel(IterParams p) {
     auto unit_pos_st = [&](int k, int& xs, int& y, bool& strt) {
       const int u = up ? uend - 1 - k : ubeg + k;
       int strip, ytop = 0;
+      if (gpool) {
+        const int m = gr1 - gr0;
+        if (k < m) {  // own segment (k == 0 primes the window)
+          strip = gs;
+          y = up ? gr1 - 1 - k : gr0 + k;
+          strt = false;
+        } else {  // pool run: the left-over segments' units gpb .. gpe - 1, strip-major
+          const int j = up ? gpe - 1 - (k - m) : gpb + (k - m);
+          const int sp = j / gHL;
+          strip = S_ - Eg + sp;
+          y = gL0 + (j - sp * gHL);
+          strt = k == m || y == (up ? H - 1 : gL0);
+        }
+        xs = strip * kTileOut - 1 + lane;
+        return;
+      }
       if (hpool) {
         const int uf = hnf * hLf;
         if (u < uf) {

@@ -217,7 +217,8 @@ def test_resvol_batch_beyond_one_call_of_trials():
     reps = -(-208 // b)
     big = {k: v.repeat(reps, *([1] * (v.dim() - 1))) for k, v in T.items()}
     with torch.no_grad():
-        R, t = m(big["img0"], big["img1"], big["depth0"], big["depth1"], big["K"])
+        R, t = m(big["img0"], big["img1"], big["depth0"], big["depth1"], big["K"], obj_mask0=big.get("mask0"),
+                 obj_mask1=big.get("mask1"))
     assert R.shape[0] == b * reps >= 208
     assert np.abs(R.cpu().numpy() - np.tile(z["R"], (reps, 1, 1))).max() < 1e-4
     assert np.abs(t.cpu().numpy().reshape(-1, 3) - np.tile(z["t"].reshape(b, 3), (reps, 1))).max() < 1e-4

@@ -26,7 +26,7 @@ p.add_argument("--from-solve", action="store_true",
                help="start from the poses of one full pyramid solve (the bench's operating point) instead of identity")
 a = p.parse_args()
 dev = torch.device("cuda:0")
-sel, levels, K = bench.make_group_inputs(a.batch, a.groups, 0, dev)
+sel, levels, K = bench.make_batches(a.batch, 0, a.groups, dev)
 if a.c4:
     for d in levels:
         d["x0"], d["x1"] = ic.pack_features(d["x0"]), ic.pack_features(d["x1"])

@@ -21,7 +21,7 @@
     }                                                                      \
   } while (0)
 
-constexpr int W = 640, H = 480, C = 32, NP = 64, STRIPS = 11, BANDS = 3;
+constexpr int W = 640, H = 480, C = 32, NP = 64, STRIPS = 11;
 typedef int v4i __attribute__((ext_vector_type(4)));
 typedef float f32x4 __attribute__((ext_vector_type(4)));
 __device__ f32x4 bload(v4i, int, int, int) __asm("llvm.amdgcn.raw.buffer.load.v4f32");
@@ -38,24 +38,41 @@ __device__ inline v4i rsrc(const void* p, uint32_t bytes) {
 
 // layout G: frame [C/G][H][W][G] floats; the 16-byte chunk k (0 .. C/4-1) of pixel (x, y)
 // lies at ((k / (G/4)) * H * W + y * W + x) * G * 4 + (k % (G/4)) * 16 bytes
-template <int G>
+// MODE 0: the marching pattern; 1: f0 only; 2: f1 taps at the pixel's own column (no
+// gather); 3: 64-column strips without halo columns (10 strips of 64); 4: grid split -- 3
+// row bands x 11 strips = 33 segments with common row cuts (neighbouring strips march the
+// same rows at the same time), wave w < 32 owns segment w, the 33rd is split 5 rows a wave
+// and marched after it; 5: as 0 without the XCD-aware workgroup remap
+template <int G, int MODE = 0>
 __global__ __launch_bounds__(256) void march(const float* f0, const float* f1, float* out, float rot, float shift) {
   __shared__ float pin[80 * 1024 / 4];  // the real kernel's LDS footprint: 2 workgroups per CU
   constexpr int NG = C / G, PER = G / 4;
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  const int task = blockIdx.x * 4 + wave;  // (pair, strip, band), band-major within a pair
-  const int b = task / (STRIPS * BANDS), rest = task % (STRIPS * BANDS);
-  if (b >= NP) return;
-  const int band = rest / STRIPS, s = rest % STRIPS;
-  const int xs = s * 62 - 1 + lane, xc = min(max(xs, 0), W - 1);
-  const int y0 = band * H / BANDS, y1 = (band + 1) * H / BANDS;
+  // the shipped schedule at 64 pairs per launch: 8 workgroups (32 waves) per pair, each
+  // wave a contiguous run of the pair's (strip, row) units in strip-major order
+  constexpr int NS = MODE == 3 ? 10 : STRIPS, NW = 32, U = NS * H;
+  // a pair's 8 workgroups on one XCD (the dispatcher deals workgroups round-robin over 8)
+  const int kb = MODE == 5 ? blockIdx.x : (blockIdx.x & 7) * (gridDim.x >> 3) + (blockIdx.x >> 3);
+  const int b = kb / 8, band = (kb % 8) * 4 + wave;
+  const int ubeg = U * band / NW, uend = U * (band + 1) / NW;
   const uint32_t frame = (uint32_t)H * W * C * 4;
   const v4i r0 = rsrc(f0 + (size_t)b * H * W * C, frame), r1 = rsrc(f1 + (size_t)b * H * W * C, frame);
   f32x4 acc = {0.f, 0.f, 0.f, 0.f};
-  for (int y = y0; y < y1; ++y) {
+  const int nunits = MODE == 4 ? 160 + 5 : uend - ubeg;
+  for (int i = 0; i < nunits; ++i) {
+    int s, y;
+    if (MODE == 4) {
+      const int seg = i < 160 ? band : 32, row = i < 160 ? i : 160 + 5 * band + (i - 160);
+      s = seg % STRIPS;
+      y = (seg / STRIPS) * 160 + (i < 160 ? row : row - 160);
+    } else {
+      s = (ubeg + i) / H;
+      y = ubeg + i - s * H;
+    }
+    const int xs = MODE == 3 ? s * 64 + lane : s * 62 - 1 + lane, xc = min(max(xs, 0), W - 1);
     const int yn = min(y + 1, H - 1);
-    const float u = xc + rot * (y - H / 2) + shift, v = y - rot * (xc - W / 2) + shift;
-    const int tx = min(max((int)floorf(u), 0), W - 2), ty = min(max((int)floorf(v) + 1, 0), H - 1);
+    const float fu = xc + rot * (y - H / 2) + shift, fv = y - rot * (xc - W / 2) + shift;
+    const int tx = MODE == 2 ? min(xc, W - 2) : min(max((int)floorf(fu), 0), W - 2), ty = min(max((int)floorf(fv) + 1, 0), H - 1);
     // all 24 loads of the row in flight in every layout (equal memory-level parallelism);
     // a group's chunks are issued back to back (same cache lines)
     f32x4 l[3 * C / 4];
@@ -65,8 +82,12 @@ __global__ __launch_bounds__(256) void march(const float* f0, const float* f1, f
 #pragma unroll
       for (int k = 0; k < PER; ++k) {
         l[3 * (g * PER + k)] = bload(r0, ((gp + yn * W + xc) * G) * 4 + 16 * k, 0, 2);
-        l[3 * (g * PER + k) + 1] = bload(r1, ((gp + ty * W + tx) * G) * 4 + 16 * k, 0, 0);
-        l[3 * (g * PER + k) + 2] = bload(r1, ((gp + ty * W + tx + 1) * G) * 4 + 16 * k, 0, 0);
+        if (MODE != 1) {
+          l[3 * (g * PER + k) + 1] = bload(r1, ((gp + ty * W + tx) * G) * 4 + 16 * k, 0, 0);
+          l[3 * (g * PER + k) + 2] = bload(r1, ((gp + ty * W + tx + 1) * G) * 4 + 16 * k, 0, 0);
+        } else {
+          l[3 * (g * PER + k) + 1] = l[3 * (g * PER + k) + 2] = f32x4{0.f, 0.f, 0.f, 0.f};
+        }
       }
     }
     asm volatile("" ::: "memory");
@@ -77,27 +98,30 @@ __global__ __launch_bounds__(256) void march(const float* f0, const float* f1, f
   if (acc.x + acc.y + acc.z + acc.w == 12345.f) out[0] = pin[(threadIdx.x + 1) & 255];
 }
 
-template <int G>
+template <int G, int MODE = 0>
 void run(const float* f0, const float* f1, float* out) {
-  const int grid = (NP * STRIPS * BANDS + 3) / 4;
+  const int grid = NP * 8;
   hipEvent_t e0, e1;
   CHECK(hipEventCreate(&e0));
   CHECK(hipEventCreate(&e1));
-  for (int i = 0; i < 5; ++i) march<G><<<grid, 256>>>(f0, f1, out, 0.05f, 0.3f);
+  for (int i = 0; i < 5; ++i) march<G, MODE><<<grid, 256>>>(f0, f1, out, 0.05f, 0.3f);
   CHECK(hipEventRecord(e0));
   const int reps = 20;
-  for (int i = 0; i < reps; ++i) march<G><<<grid, 256>>>(f0, f1, out, 0.05f, 0.3f);
+  for (int i = 0; i < reps; ++i) march<G, MODE><<<grid, 256>>>(f0, f1, out, 0.05f, 0.3f);
   CHECK(hipEventRecord(e1));
   CHECK(hipEventSynchronize(e1));
   float ms;
   CHECK(hipEventElapsedTime(&ms, e0, e1));
   const double us = ms * 1e3 / reps;
   const double alg = 2.0 * NP * H * W * C * 4;  // f0 + f1 once each
-  printf("G=%2d (%s): %7.1f us per launch, %6.0f GB/s algorithmic (f0 + f1)\n", G,
-         G == 4 ? "channel quads" : G == 32 ? "NHWC" : "channel groups", us, alg / (us * 1e-6) / 1e9);
+  static const char* modes[] = {"marching", "f0 only", "f1 at own column", "64-col strips", "grid 3x11 + pool",
+                                "no XCD remap"};
+  printf("G=%2d %-17s: %7.1f us per launch, %6.0f GB/s algorithmic (f0 + f1)\n", G, modes[MODE], us,
+         (MODE == 1 ? alg / 2 : alg) / (us * 1e-6) / 1e9);
 }
 
-int main() {
+int main(int argc, char** argv) {
+  const int only = argc > 1 ? atoi(argv[1]) : -1;  // one G = 4 mode (for a PMC pass), or all
   const size_t n = (size_t)NP * C * W * H;
   float *f0, *f1, *out;
   CHECK(hipMalloc(&f0, n * 4));
@@ -105,11 +129,27 @@ int main() {
   CHECK(hipMalloc(&out, 4));
   CHECK(hipMemset(f0, 0, n * 4));
   CHECK(hipMemset(f1, 0, n * 4));
+  if (only >= 0) {
+    switch (only) {
+      case 0: run<4, 0>(f0, f1, out); break;
+      case 1: run<4, 1>(f0, f1, out); break;
+      case 2: run<4, 2>(f0, f1, out); break;
+      case 3: run<4, 3>(f0, f1, out); break;
+      case 4: run<4, 4>(f0, f1, out); break;
+      default: run<4, 5>(f0, f1, out); break;
+    }
+    return 0;
+  }
   for (int rep = 0; rep < 2; ++rep) {
     run<4>(f0, f1, out);
     run<8>(f0, f1, out);
     run<16>(f0, f1, out);
     run<32>(f0, f1, out);
+    run<4, 1>(f0, f1, out);
+    run<4, 2>(f0, f1, out);
+    run<4, 3>(f0, f1, out);
+    run<4, 4>(f0, f1, out);
+    run<4, 5>(f0, f1, out);
   }
   return 0;
 }
