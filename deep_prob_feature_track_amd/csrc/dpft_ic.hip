@@ -359,7 +359,7 @@ struct IterParams {
   const float* wgt;      // NO_UNCERTAINTY: per-pixel M-estimator weights [B,1,H,W] (nullable)
   const float* depth0;   // COMBINE_ICP: raw depth pyramids level (max-pooled), [B,1,H,W]
   const float* depth1;
-  const float* nrm1;     // COMBINE_ICP: normal map of frame 1, [B,3,H,W] (workspace, per level)
+  const f32x4* nrm1;     // COMBINE_ICP: frame 1's [nx, ny, nz, depth1] map, [B,H,W] (workspace, per level)
   float icp_w;           // ScaleNet('None') weight (algorithms.py:1563)
   const float* K;
   const float* R;
@@ -562,7 +562,9 @@ struct QuadLoadsR {
 // ============================================================ ICP term (combine_ICP)
 // Point-to-plane residual and inverse Jacobian of one pixel, ScaleNet('None')
 // weight applied (algorithms.py:916-997, 668-689; geometry.py:1129-1136).
-// Frame 1's normal map is pose-independent and comes from icp_normals_kernel.
+// Frame 1's normal map is pose-independent and comes from icp_normals_kernel, interleaved
+// with frame 1's depth: one 16-byte [nx, ny, nz, depth1] element per pixel, so a tap is
+// one load instead of four scalar gathers (same values, same arithmetic: same bits).
 struct IcpTerm {
   float J[6];  // w * J (already the reference's negated, sigma-normalised J)
   float r;     // w * r (1e-6 * w where occluded)
@@ -571,8 +573,7 @@ struct IcpTerm {
 
 __device__ __forceinline__ IcpTerm icp_pixel(float xr, float yr, float d0, const float* __restrict__ Rm,
                                              const float* __restrict__ tv, float fx, float fy, float cx, float cy,
-                                             int H, int W, const float* __restrict__ dep1,
-                                             const float* __restrict__ nrm1, int HW, bool mask0_bg,
+                                             int H, int W, const f32x4* __restrict__ nd1, bool mask0_bg,
                                              const uint8_t* __restrict__ m1b, float wgt) {
 #pragma clang fp contract(off)
   // vertex0 = [px, py, 1] * depth0; P = R V0 + t (CPU bmm order, then + t)
@@ -586,13 +587,15 @@ __device__ __forceinline__ IcpTerm icp_pixel(float xr, float yr, float d0, const
   int x0, x1, y0, y1;
   const Taps tp = make_taps_xy(u, v, H, W, x0, x1, y0, y1);
   // vertex1 sampled: the vertex map at the four taps, then the sampler's chain
-  const float a = dep1[tp.o00], b = dep1[tp.o01], c = dep1[tp.o10], d = dep1[tp.o11];
+  const f32x4 q00 = nd1[tp.o00], q01 = nd1[tp.o01], q10 = nd1[tp.o10], q11 = nd1[tp.o11];
+  const float a = q00.w, b = q01.w, c = q10.w, d = q11.w;
   const float px0 = ((float)x0 - cx) / fx, px1 = ((float)x1 - cx) / fx;
   const float py0 = ((float)y0 - cy) / fy, py1 = ((float)y1 - cy) / fy;
   const float V1x = bil4(px0 * a, px1 * b, px0 * c, px1 * d, tp);
   const float V1y = bil4(py0 * a, py0 * b, py1 * c, py1 * d, tp);
   const float V1z = bil4(a, b, c, d, tp);
-  const float Nx = bil(nrm1, tp), Ny = bil(nrm1 + HW, tp), Nz = bil(nrm1 + 2 * HW, tp);
+  const float Nx = bil4(q00.x, q01.x, q10.x, q11.x, tp), Ny = bil4(q00.y, q01.y, q10.y, q11.y, tp);
+  const float Nz = bil4(q00.z, q01.z, q10.z, q11.z, tp);
   const float Dx = Px - V1x, Dy = Py - V1y, Dz = Pz - V1z;
   bool occ = !inview || (sqrtf((Dx * Dx + Dy * Dy) + Dz * Dz) > 0.1f) || mask0_bg;
   if (m1b) occ = occ || !(bil_u8(m1b, tp) > 0.0f);
@@ -621,12 +624,13 @@ __device__ __forceinline__ IcpTerm icp_pixel(float xr, float yr, float d0, const
 
 // Frame-1 normal map of one level (algorithms.py:2148-2172): vertex map
 // (geometry.py:1129-1136), unnormalised replicate-padded Sobel, cross product,
-// / (|n| + 1e-8), zero where depth equals the batch-global min or max.
+// / (|n| + 1e-8), zero where depth equals the batch-global min or max; stored as
+// [B][H][W] x [nx, ny, nz, depth1] (the depth beside its normal for icp_pixel's taps).
 // `dext`: order-encoded (min, max) word pairs, one per independent batch of `group` pairs
 // (DPFT_GROUP; group = B: the call is one batch, the reference's batch-global extrema).
 __global__ __launch_bounds__(kThreads) void icp_normals_kernel(const float* __restrict__ depth, const float* __restrict__ K,
                                                                int B, int H, int W, const uint32_t* __restrict__ dext,
-                                                               int group, float* __restrict__ nrm) {
+                                                               int group, f32x4* __restrict__ nrm) {
   const int HW = H * W;
   const long i = (long)blockIdx.x * kThreads + threadIdx.x;
   if (i >= (long)B * HW) return;
@@ -655,9 +659,7 @@ __global__ __launch_bounds__(kThreads) void icp_normals_kernel(const float* __re
   const float mag = sqrtf((n[0] * n[0] + n[1] * n[1]) + n[2] * n[2]) + 1e-8f;
   const float d = db[pix];
   const bool bad = d == dec_ord(dext[0]) || d == dec_ord(dext[1]);
-  float* o = nrm + (size_t)b * 3 * HW + pix;
-#pragma unroll
-  for (int c = 0; c < 3; ++c) o[(size_t)c * HW] = bad ? 0.0f : n[c] / mag;
+  nrm[i] = bad ? f32x4{0.0f, 0.0f, 0.0f, d} : f32x4{n[0] / mag, n[1] / mag, n[2] / mag, d};
 }
 
 // ============================================================ last-block finalize
@@ -1263,8 +1265,7 @@ __global__ __launch_bounds__(kThreads, 1) void ic_reduce_kernel(IterParams p) {
         const int yr = F.y0 + r;
         const float d0v = p.depth0[(size_t)b * HW + yr * W + F.xc];
         const IcpTerm ic = icp_pixel(F.wp[r].xr, F.wp[r].yr, d0v, Rm, tv, fx, fy, cx, cy, H, W,
-                                     p.depth1 + (size_t)b * HW, p.nrm1 + (size_t)b * 3 * HW, HW, !F.m0[r], m1b,
-                                     p.icp_w);
+                                     p.nrm1 + (size_t)b * HW, !F.m0[r], m1b, p.icp_w);
         int kq2 = 0;
 #pragma unroll
         for (int i = 0; i < 6; ++i) {
@@ -2293,8 +2294,7 @@ __global__ __launch_bounds__(kThreads) void ic_residual_kernel(IterParams p) {
     if (tru) inv = inv || (s00 == g0min) || (s00 == g0max);
     if (ICP) {  // forward_residuals: ICP without object masks, combined occlusion (algorithms.py:765-782)
       const IcpTerm ic = icp_pixel(px.xr, px.yr, p.depth0[(size_t)b * HW + pix], Rm, tv, fx, fy, cx, cy, H, W,
-                                   p.depth1 + (size_t)b * HW, p.nrm1 + (size_t)b * 3 * HW, HW, false, nullptr,
-                                   p.icp_w);
+                                   p.nrm1 + (size_t)b * HW, false, nullptr, p.icp_w);
       inv = inv || ic.occ;
       srr = srr + ic.r * ic.r;
     }
@@ -2690,10 +2690,10 @@ size_t rec_bytes(const DpftLevelDesc& d) {
   return (slots * kRec * sizeof(float) + 255) & ~(size_t)255;
 }
 
-// COMBINE_ICP: frame-1 normal map [B,3,H,W] between the pair records and the
+// COMBINE_ICP: frame-1 normal + depth map [B,H,W,4] between the pair records and the
 // workgroup records (the latter grow with the number of poses of a residual call)
 size_t nrm_bytes(const DpftLevelDesc& d) {
-  return (d.flags & DPFT_COMBINE_ICP) ? (size_t)d.B * 3 * d.H * d.W * sizeof(float) : 0;
+  return (d.flags & DPFT_COMBINE_ICP) ? (size_t)d.B * 4 * d.H * d.W * sizeof(float) : 0;
 }
 
 size_t ws_need(const DpftLevelDesc& d) {
@@ -2723,7 +2723,7 @@ IterParams make_params(const DpftLevelDesc& d, const DpftLevelTensors& tt, const
   p.wgt = tt.weights;
   p.depth0 = tt.depth0;
   p.depth1 = tt.depth1;
-  p.nrm1 = (d.flags & DPFT_COMBINE_ICP) ? reinterpret_cast<const float*>(static_cast<char*>(ws) + nrm_offset(d))
+  p.nrm1 = (d.flags & DPFT_COMBINE_ICP) ? reinterpret_cast<const f32x4*>(static_cast<char*>(ws) + nrm_offset(d))
                                         : nullptr;
   p.icp_w = d.icp_weight;
   p.K = tt.K;
@@ -2820,7 +2820,7 @@ int launch_minmax(const DpftLevelDesc& d, const DpftLevelTensors& tt, void* ws, 
       return rc;
     }
     const size_t n = (size_t)d.B * d.H * d.W;
-    float* nrm = reinterpret_cast<float*>(static_cast<char*>(ws) + nrm_offset(d));
+    f32x4* nrm = reinterpret_cast<f32x4*>(static_cast<char*>(ws) + nrm_offset(d));
     hipLaunchKernelGGL(icp_normals_kernel, dim3((unsigned)((n + kThreads - 1) / kThreads)), dim3(kThreads), 0, st,
                        tt.depth1, tt.K, d.B, d.H, d.W, ctrl + word, gs, nrm);
     if ((rc = hip_check("icp_normals_kernel"))) return rc;
