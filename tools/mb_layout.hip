@@ -42,7 +42,8 @@ __device__ inline v4i rsrc(const void* p, uint32_t bytes) {
 // gather); 3: 64-column strips without halo columns (10 strips of 64); 4: grid split -- 3
 // row bands x 11 strips = 33 segments with common row cuts (neighbouring strips march the
 // same rows at the same time), wave w < 32 owns segment w, the 33rd is split 5 rows a wave
-// and marched after it; 5: as 0 without the XCD-aware workgroup remap
+// and marched after it; 5: as 0 without the XCD-aware workgroup remap; 6: as 4 with a
+// workgroup barrier every row (the 4 waves -- mostly 4 adjacent strips -- in lockstep)
 template <int G, int MODE = 0>
 __global__ __launch_bounds__(256) void march(const float* f0, const float* f1, float* out, float rot, float shift) {
   __shared__ float pin[80 * 1024 / 4];  // the real kernel's LDS footprint: 2 workgroups per CU
@@ -58,10 +59,12 @@ __global__ __launch_bounds__(256) void march(const float* f0, const float* f1, f
   const uint32_t frame = (uint32_t)H * W * C * 4;
   const v4i r0 = rsrc(f0 + (size_t)b * H * W * C, frame), r1 = rsrc(f1 + (size_t)b * H * W * C, frame);
   f32x4 acc = {0.f, 0.f, 0.f, 0.f};
-  const int nunits = MODE == 4 ? 160 + 5 : uend - ubeg;
+  constexpr bool GP = MODE == 4 || MODE == 6;
+  const int nunits = GP ? 160 + 5 : uend - ubeg;
   for (int i = 0; i < nunits; ++i) {
     int s, y;
-    if (MODE == 4) {
+    if (MODE == 6) __syncthreads();
+    if (GP) {
       const int seg = i < 160 ? band : 32, row = i < 160 ? i : 160 + 5 * band + (i - 160);
       s = seg % STRIPS;
       y = (seg / STRIPS) * 160 + (i < 160 ? row : row - 160);
@@ -115,7 +118,7 @@ void run(const float* f0, const float* f1, float* out) {
   const double us = ms * 1e3 / reps;
   const double alg = 2.0 * NP * H * W * C * 4;  // f0 + f1 once each
   static const char* modes[] = {"marching", "f0 only", "f1 at own column", "64-col strips", "grid 3x11 + pool",
-                                "no XCD remap"};
+                                "no XCD remap", "grid + row barrier"};
   printf("G=%2d %-17s: %7.1f us per launch, %6.0f GB/s algorithmic (f0 + f1)\n", G, modes[MODE], us,
          (MODE == 1 ? alg / 2 : alg) / (us * 1e-6) / 1e9);
 }
@@ -136,7 +139,8 @@ int main(int argc, char** argv) {
       case 2: run<4, 2>(f0, f1, out); break;
       case 3: run<4, 3>(f0, f1, out); break;
       case 4: run<4, 4>(f0, f1, out); break;
-      default: run<4, 5>(f0, f1, out); break;
+      case 5: run<4, 5>(f0, f1, out); break;
+      default: run<4, 6>(f0, f1, out); break;
     }
     return 0;
   }
@@ -150,6 +154,7 @@ int main(int argc, char** argv) {
     run<4, 3>(f0, f1, out);
     run<4, 4>(f0, f1, out);
     run<4, 5>(f0, f1, out);
+    run<4, 6>(f0, f1, out);
   }
   return 0;
 }

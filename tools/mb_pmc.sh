@@ -2,7 +2,7 @@
 # FETCH_SIZE per launch of tools/mb_layout's G=4 modes (one rocprofv3 pass per mode)
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 export TMPDIR=/tmp
-for m in 0 1 3 4; do
+for m in 0 3 4 6; do
   d=gpurun_out/mb_pmc/m$m
   timeout -s KILL 60 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $d -o c -- ./tools/mb_layout $m > /dev/null 2>&1 || exit 1
   python - "$d" "$m" <<'PY'
