@@ -80,6 +80,7 @@ constexpr int kMaxSteps = 4;           // tile paths: up to 4 * kMaxSteps rows p
 constexpr long kSplitMaxPixels = DPFT_SPLIT_MAX_PIXELS;
 constexpr long kSplitMaxLaunchPixels = DPFT_SPLIT_MAX_LAUNCH_PIXELS;
 constexpr int kMarchSkew = DPFT_MARCH_SKEW;  // band-size skew of the marching schedule (64ths, 0..63)
+constexpr int kMarchMinRows = DPFT_MARCH_MIN_ROWS;  // marching: minimum rows per wave (0: none)
 constexpr int kRingQ = DPFT_RING_Q;          // marching quad loop: quads in flight (kRingQ - 1 ahead)
 constexpr int kF0Aux = 2;                    // cache policy of the marching f0 stream (nt: used once)
 constexpr int kGridWaste = 4;                // marching band grid: idle waves allowed (64ths of a pair's)
@@ -2857,6 +2858,11 @@ int launch_reduce_k(IterParams p, hipStream_t st) {
   if (cap <= 0) return fail(DPFT_E_HIP, "occupancy query failed");
   p.nbpp = std::max(1, std::min(cap / p.B, p.per_pair));  // one dispatch round
   if ((long)p.B * p.nbpp > kMaxGrid) p.nbpp = std::max(1, kMaxGrid / p.B);
+  if (C4 && CT > 0 && kMarchMinRows > 0) {  // marching: at most one wave per kMarchMinRows units
+    constexpr int mr = kMarchMinRows > 0 ? kMarchMinRows : 1;
+    const long waves = ((long)p.tiles_x * p.H + mr - 1) / mr;
+    p.nbpp = std::max(1, std::min(p.nbpp, (int)((waves + 3) / 4)));
+  }
   p.round_wg = cap / 8;
   p.fin.nbpp = p.nbpp;
   // the finalize runs in-kernel (last-workgroup handshake, fin_on)

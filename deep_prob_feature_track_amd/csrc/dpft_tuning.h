@@ -17,6 +17,11 @@
 #ifndef DPFT_MARCH_SKEW
 #define DPFT_MARCH_SKEW 10
 #endif
+// marching bands: at least this many rows per wave (0: no minimum) -- fewer workgroups per
+// pair on short levels, whose bands otherwise spend two window rows of priming per band
+#ifndef DPFT_MARCH_MIN_ROWS
+#define DPFT_MARCH_MIN_ROWS 0
+#endif
 // marching quad loop: quads in flight (swept 2 / 3 / 4 / 6)
 #ifndef DPFT_RING_Q
 #define DPFT_RING_Q 4
