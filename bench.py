@@ -66,12 +66,17 @@ def parse():
 # ---------------------------------------------------------------------------- inputs
 def make_batches(B, first, count, device, icp=False):
     """`count` consecutive independent batches of B pairs, batch q (q = first .. first +
-    count - 1) holding ordered pairs q B .. q B + B - 1 (cycled through the 20 of the five
-    frames), stacked along the pair axis: (pairs, per-level NCHW dicts, K [count B, 4])."""
+    count - 1) holding stream pairs q B .. q B + B - 1, stacked along the pair axis:
+    (pairs, per-level NCHW dicts, K [count B, 4]).  Stream pair n is ordered pair n mod 20
+    of the five frames with flip code (n div 20) mod 4 (left-right / up-down, both frames
+    alike: recipe.flip_case), so the cfg3 batch of 64 holds 64 distinct pairs (SURVEY.md
+    8d); pairs 0..19 are unflipped (the reference fixture of batch 0)."""
     import recipe
+    n_ord = len(recipe.ORDERED_PAIRS)
     sel, levels = [], [dict() for _ in range(LEVELS)]
     for q in range(first, first + count):
-        bsel = [recipe.ORDERED_PAIRS[(q * B + k) % len(recipe.ORDERED_PAIRS)] for k in range(B)]
+        bsel = [recipe.ORDERED_PAIRS[(q * B + k) % n_ord] for k in range(B)]
+        flips = [((q * B + k) // n_ord) % 4 for k in range(B)]
         sel += bsel
         d0 = [recipe.depth_m(i) for i, _ in bsel]
         d1 = [recipe.depth_m(j) for _, j in bsel]
@@ -87,6 +92,13 @@ def make_batches(B, first, count, device, icp=False):
                 part["depth0"] = recipe.max_pool(np.stack(d0)[:, None], k)
                 part["depth1"] = recipe.max_pool(np.stack(d1)[:, None], k)
             for key, v in part.items():
+                if any(flips):
+                    v = v.copy()  # (level 0's max_pool may return its input, shared by all levels)
+                for b, code in enumerate(flips):
+                    if code & 1:
+                        v[b] = v[b][..., ::-1].copy()
+                    if code & 2:
+                        v[b] = v[b][..., ::-1, :].copy()
                 levels[l].setdefault(key, []).append(v)
     dev = lambda a: torch.from_numpy(np.ascontiguousarray(np.concatenate(a))).to(device)
     levels = [{k: dev(v) for k, v in d.items()} for d in levels]
@@ -473,7 +485,8 @@ def main():
             "value": value, "unit": "IC iterations/s (all levels, 12 per pair)",
             "n_gpus": world, "steps": a.steps, "warmup": a.warmup, "ms_per_step": ms_per_step,
             "higher_is_better": True, "scaling": "weak" if weak else "strong", "vs_baseline": None, "dtype": "f32",
-            "data": "synthetic: deterministic triangle-wave features of the 5 TUM fr1/desk example frames "
+            "data": "synthetic: deterministic triangle-wave features of the 5 TUM fr1/desk example frames, "
+                    "the 20 ordered pairs cycled with a left-right / up-down flip per round of 20 (distinct pairs) "
                     "(tests/golden/recipe.py; trained checkpoints absent)",
             "config": {"workload": ("cfg5: " if a.icp else "cfg3: ") +
                                    ("eval stream of global batches of %d pairs, " % per_step if not weak else
@@ -485,6 +498,7 @@ def main():
                        "parallelism": f"pair-sharded x{world}, RCCL all-gather of poses",
                        "graph": not a.no_graph, "feature_layout": a.layout, "setup_warm_ms": a.setup_warm_ms},
             "latency_ms_per_step": latency_ms,
+            "latency_what": f"one step alone on rank 0: its {n_r} pairs, 4 levels x 3 iterations, nothing else in flight",
             "pairs_per_s": per_step * a.steps / elapsed,
             "l0_iters_per_s": per_step * ITERS * a.steps / elapsed,
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
