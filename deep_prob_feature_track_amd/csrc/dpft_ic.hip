@@ -83,7 +83,7 @@ constexpr int kMarchSkew = DPFT_MARCH_SKEW;  // band-size skew of the marching s
 constexpr int kMarchMinRows = DPFT_MARCH_MIN_ROWS;  // marching: minimum rows per wave (0: none)
 constexpr int kRingQ = DPFT_RING_Q;          // marching quad loop: quads in flight (kRingQ - 1 ahead)
 constexpr int kF0Aux = 2;                    // cache policy of the marching f0 stream (nt: used once)
-constexpr int kGridWaste = 4;                // marching band grid: idle waves allowed (64ths of a pair's)
+constexpr int kGridWaste = DPFT_GRID_WASTE;  // marching band grid: idle waves allowed (64ths of a pair's)
 
 // ---- reduce-record layout (floats) ------------------------------------------
 constexpr int kRec = 48;

@@ -17,6 +17,11 @@
 #ifndef DPFT_MARCH_SKEW
 #define DPFT_MARCH_SKEW 10
 #endif
+// marching band grid: idle waves allowed, in 64ths of a pair's waves (more idle waves than
+// this and the hybrid or grid + pool split is used instead)
+#ifndef DPFT_GRID_WASTE
+#define DPFT_GRID_WASTE 4
+#endif
 // marching bands: at least this many rows per wave (0: no minimum) -- fewer workgroups per
 // pair on short levels, whose bands otherwise spend two window rows of priming per band
 #ifndef DPFT_MARCH_MIN_ROWS
