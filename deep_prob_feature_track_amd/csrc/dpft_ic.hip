@@ -534,6 +534,16 @@ __device__ __forceinline__ float lane_from_right(float v) {  // lane l gets lane
 }
 
 // Unit-normalised Sobel from the three rows of this lane's column (algorithms.py:1852-1863).
+// c ? a : b for a wave-uniform c, always as one v_cndmask: a select whose operand is a
+// load can otherwise become a branch, and the copies on its two paths wait for every load
+// in flight (the waitcnt pass cannot tell which path issued what)
+__device__ __forceinline__ float sel_uniform(bool c, float a, float b) {
+  float r;
+  const uint32_t m = (uint32_t)__builtin_amdgcn_readfirstlane(c ? -1 : 0);  // in SGPRs
+  asm("v_cndmask_b32 %0, %2, %1, %3" : "=v"(r) : "v"(a), "v"(b), "s"(((uint64_t)m << 32) | m));
+  return r;
+}
+
 __device__ __forceinline__ void sobel_cols(float top, float mid, float bot, float& gx, float& gy) {
   const float V = top + 2.0f * mid + bot;
   const float D = bot - top;
@@ -1467,17 +1477,31 @@ __global__ __launch_bounds__(kThreads, 1) void ic_reduce_kernel(IterParams p) {
     f32x4 tc[NQW][2];
     int tc_ob = -1;
 
-    // d of the next step's (up to) two rows, prefetched one step ahead
-    float dnx[2] = {0.f, 0.f};
-    auto load_d2 = [&](int k, float (&dd)[2]) {
-#pragma unroll
-      for (int r = 0; r < 2; ++r) {
-        int xs, y;
-        unit_pos(min(k + r, nrows - 1), xs, y);
-        dd[r] = bld(rd0, y * W * 4 + min(max(xs, 0), W - 1) * 4, 0);
-      }
+    // inverse depth of the next step's pixel, prefetched one step ahead
+    float dnx = 0.f;
+    auto load_dpx = [&](int xs, int y) { return bld(rd0, y * W * 4 + min(max(xs, 0), W - 1) * 4, 0); };
+    constexpr int RM = kRingQ < NQW ? kRingQ : NQW;
+    static_assert(RM >= 2 && RM <= NQW && NQW % RM == 0, "ring depth");
+    QuadM L[RM];
+    // f0 row y + dir of a step's first RM - 1 quads depends on the row only: the previous
+    // step issues it into the ring slots its last quads free, so it streams during that
+    // step's epilogue and this step's frame (warp, gathers).  (A loop-carried sigma0 row
+    // load the same way gets a copy at the loop edge, and the copy waits for every load.)
+    // (not with combine_ICP: its per-pixel term leaves no registers for the loop-carried
+    // rows -- 256 VGPRs, one wave per SIMD; there the first quads' f0 rows are issued at the
+    // start of their own step, before the frame)
+    constexpr bool kPf = !ICP;
+    auto prefetch_f = [&](int i, int colq, int yn) {
+      L[i].f = llvm_buf_load_f32x4(rf0, colq, i * 4 * (int)planeB + yn * W * 16, kF0Aux);
     };
-    if (nrows > 0) load_d2(0, dnx);
+    if (nrows > 0) {
+      int xs0, y0;
+      unit_pos(0, xs0, y0);
+      dnx = load_dpx(xs0, y0);
+#pragma unroll
+      for (int i = 0; i < RM - 1; ++i)
+        if (kPf) prefetch_f(i, min(max(xs0, 0), W - 1) * 16, min(max(y0 + dir, 0), H - 1));
+    }
     // One marching step: row y of the wave's strip.  Window slots (LDS): slot 0 = row
     // y - dir, slot 1 = row y; quad q reads both and leaves (y, y + dir) for the next step.
     // The quad loop is straight-line with static quad indices (the tap cache lives in
@@ -1486,8 +1510,7 @@ __global__ __launch_bounds__(kThreads, 1) void ic_reduce_kernel(IterParams p) {
       int xs, y;
       bool strt0;
       unit_pos_st(k, xs, y, strt0);
-      const float dcur = dnx[0];
-      if (k + 1 < nrows) load_d2(k + 1, dnx);
+      const float dcur = dnx;
       const int colq = min(max(xs, 0), W - 1) * 16;
       if (k == 0 || strt0) {  // prime the window: rows y - dir (replicate-clamped) and y
         const int yp = min(max(y - dir, 0), H - 1);
@@ -1501,31 +1524,45 @@ __global__ __launch_bounds__(kThreads, 1) void ic_reduce_kernel(IterParams p) {
           sprev = bld(rs0, colq >> 2, yp * W * 4);
           scur = bld(rs0, colq >> 2, y * W * 4);
         }
+        // drain here (strip starts only): otherwise the wait counts after the join are the
+        // conservative ones of this path, and every row-step waits for its prefetched rows
+        __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0)
       }
       const int yn = min(max(y + dir, 0), H - 1);
+      auto issue_f = [&](QuadM& Qm, int q) {
+        Qm.f = llvm_buf_load_f32x4(rf0, colq, q * 4 * (int)planeB + yn * W * 16, kF0Aux);
+      };
+      if (!kPf) {
+#pragma unroll
+        for (int i = 0; i < RM - 1; ++i) issue_f(L[i], i);
+      }
+      const float snew = (CS1 && !NOSIG) ? bld(rs0, colq >> 2, yn * W * 4) : 0.f;
+      // the next step's (after the last step: this one's again, so that the loads are
+      // unconditional -- a load under a branch makes the wait counts of every later quad
+      // conservative)
+      int xs1, y1;
+      unit_pos(min(k + 1, nrows - 1), xs1, y1);
+      const int colq1 = min(max(xs1, 0), W - 1) * 16, yn1 = min(max(y1 + dir, 0), H - 1);
       Frame F;
       {
         const float dv[1] = {dcur};
         make_frame_xy(xs, y, dv, F, false);
       }
-      const float snew = (CS1 && !NOSIG) ? bld(rs0, colq >> 2, yn * W * 4) : 0.f;
-      constexpr int RM = kRingQ < NQW ? kRingQ : NQW;
-      static_assert(RM >= 2 && RM <= NQW, "ring depth");
-      QuadM L[RM];
+      // after the frame has consumed dcur: the new load then reuses its registers (a
+      // loop-carried copy of a register with a load in flight would wait for every load)
+      dnx = load_dpx(xs1, y1);  // unconditional (clamped to the last row): no phi of the old value
       // tap cache: trailing / leading pair bases and weights of this row
       const int obT = up ? F.tp[0].ob1 : F.tp[0].ob0, obL = up ? F.tp[0].ob0 : F.tp[0].ob1;
       const bool tc_hit = obT == tc_ob;
-      PairWeights wq = F.pw[0];  // channel-unit weights of slots t[0..3]
+      PairWeights wq;  // channel-unit weights of slots t[0..3]
       tc_ob = obL;
-      if (up) {  // slots 0/1 hold the trailing pair: the lower row when marching up
-        wq.w0 = F.pw[0].w2;
-        wq.w1 = F.pw[0].w3;
-        wq.w2 = F.pw[0].w0;
-        wq.w3 = F.pw[0].w1;
-      }
-      auto issue = [&](QuadM& Qm, int q) {
+      // slots 0/1 hold the trailing pair: the lower row when marching up
+      wq.w0 = sel_uniform(up, F.pw[0].w2, F.pw[0].w0);
+      wq.w1 = sel_uniform(up, F.pw[0].w3, F.pw[0].w1);
+      wq.w2 = sel_uniform(up, F.pw[0].w0, F.pw[0].w2);
+      wq.w3 = sel_uniform(up, F.pw[0].w1, F.pw[0].w3);
+      auto issue_t = [&](QuadM& Qm, int q) {
         const int po = q * 4 * (int)planeB;
-        Qm.f = llvm_buf_load_f32x4(rf0, colq, po + yn * W * 16, kF0Aux);
         // branch-free: a hit lane re-requests its leading pair (an L1 hit next to the
         // leading loads below) and selects the cached bytes; a divergent branch around
         // the loads would make the waitcnt bookkeeping wait on the next quad's loads
@@ -1537,17 +1574,7 @@ __global__ __launch_bounds__(kThreads, 1) void ic_reduce_kernel(IterParams p) {
         Qm.t[3] = bld4(rf1, obL * 16 + 16, po);
       };
 #pragma unroll
-      for (int i = 0; i < RM - 1; ++i) issue(L[i], i);
-      if (CS1 && !NOSIG) {
-        // sigma0 rows top / centre / bottom (marching direction folded in)
-        F.s0r[0] = up ? snew : sprev;
-        F.s0r[1] = scur;
-        F.s0r[2] = up ? sprev : snew;
-        sprev = scur;
-        scur = snew;
-      }
-      PixelTerms T;
-      pixel_terms(F, T);
+      for (int i = 0; i < RM - 1; ++i) issue_t(L[i], i);
       f32x2 Q[9];
 #pragma unroll
       for (int i = 0; i < 9; ++i) Q[i] = f32x2{0.f, 0.f};
@@ -1603,9 +1630,27 @@ __global__ __launch_bounds__(kThreads, 1) void ic_reduce_kernel(IterParams p) {
       // each unit's accumulators are pinned at its end (unitc), so the rounds keep this order
 #pragma unroll
       for (int qq = 0; qq < NQW; ++qq) {
-        if (qq + RM - 1 < NQW) issue(L[(qq + RM - 1) % RM], qq + RM - 1);
+        if (qq + RM - 1 < NQW) {
+          issue_f(L[(qq + RM - 1) % RM], qq + RM - 1);
+          issue_t(L[(qq + RM - 1) % RM], qq + RM - 1);
+        } else if (kPf) {  // the next step's quad qq + RM - 1 - NQW into the freed slot
+          prefetch_f(qq + RM - 1 - NQW, colq1, yn1);
+        }
         unitc(qq, L[qq % RM]);
       }
+      // the frame's gathers and the sigma0 row are resolved after the channel loop (a
+      // select of a loaded value under the wave-uniform direction becomes a branch whose
+      // copies wait for every load in flight, before the first tap is issued)
+      if (CS1 && !NOSIG) {
+        // sigma0 rows top / centre / bottom (marching direction folded in)
+        F.s0r[0] = sel_uniform(up, snew, sprev);
+        F.s0r[1] = scur;
+        F.s0r[2] = sel_uniform(up, sprev, snew);
+        sprev = scur;
+        scur = snew;
+      }
+      PixelTerms T;
+      pixel_terms(F, T);
       Sums S;
       float q[9];
 #pragma unroll
