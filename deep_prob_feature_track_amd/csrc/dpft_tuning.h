@@ -13,9 +13,10 @@
 #define DPFT_SPLIT_MAX_LAUNCH_PIXELS 320000
 #endif
 // marching bands: weights 64 + skew / 64 - skew for the first / second dispatched half of a
-// pair's waves (swept 0..22 in rounds 1-2; 10 fastest)
+// pair's waves (swept 0..22 in rounds 1-2: 10 fastest; round 3 with the cross-row f0
+// prefetch, 64 pairs per launch: 0..3 fastest, within 0.5 % of each other, 10 -1.3 %)
 #ifndef DPFT_MARCH_SKEW
-#define DPFT_MARCH_SKEW 10
+#define DPFT_MARCH_SKEW 2
 #endif
 // marching band grid: idle waves allowed, in 64ths of a pair's waves (more idle waves than
 // this and the hybrid or grid + pool split is used instead)
