@@ -1465,7 +1465,8 @@ __global__ __launch_bounds__(kThreads, 1) void ic_reduce_kernel(IterParams p) {
     float sprev = 0.f, scur = 0.f;
     struct QuadM {
       f32x4 f;      // f0 row y + dir
-      f32x4 t[4];   // f1 taps (see gather4 / QuadLoadsR); tap cache: trailing pair, leading pair
+      f32x4 t[2];   // f1 trailing tap pair (on a tap-cache hit: a re-request of the leading pair)
+      f32x4 P;      // partial residual of the cached trailing pair (see issue_t)
     };
     // Tap cache: in marching order, the f1 tap row a pixel row shares with
     // the next one is its LEADING row (lower row marching down, upper row marching up)
@@ -1476,6 +1477,8 @@ __global__ __launch_bounds__(kThreads, 1) void ic_reduce_kernel(IterParams p) {
     // otherwise misses the XCD's L2 one row-step later.
     f32x4 tc[NQW][2];
     int tc_ob = -1;
+#pragma unroll
+    for (int q = 0; q < NQW; ++q) tc[q][0] = tc[q][1] = f32x4{0.f, 0.f, 0.f, 0.f};  // weighted 0 until cached
 
     // inverse depth of the next step's pixel, prefetched one step ahead
     float dnx = 0.f;
@@ -1561,17 +1564,27 @@ __global__ __launch_bounds__(kThreads, 1) void ic_reduce_kernel(IterParams p) {
       wq.w1 = sel_uniform(up, F.pw[0].w3, F.pw[0].w1);
       wq.w2 = sel_uniform(up, F.pw[0].w0, F.pw[0].w2);
       wq.w3 = sel_uniform(up, F.pw[0].w1, F.pw[0].w3);
+      // Tap weights split by the cache: on a hit the cached trailing pair carries the
+      // trailing weights (w0h, w1h) and the loaded one 0; on a miss the other way round.
+      const float w0h = tc_hit ? wq.w0 : 0.f, w1h = tc_hit ? wq.w1 : 0.f;
+      const float w0m = tc_hit ? 0.f : wq.w0, w1m = tc_hit ? 0.f : wq.w1;
       auto issue_t = [&](QuadM& Qm, int q) {
         const int po = q * 4 * (int)planeB;
+        // The cached trailing pair of quad q is consumed here, before the new leading pair
+        // is loaded into its registers (no copy of the cache per row):
+        // P = w1h tc1 + (w0h tc0 - fm), fm = f0 row y from the window -- the first two terms
+        // of the residual, in the order the residual sums them (below).  On a miss P = -fm.
+        const f32x4 fm = win[(NQW + q) * 64 + lane];
+        Qm.P = __builtin_elementwise_fma(f32x4{w1h, w1h, w1h, w1h}, tc[q][1],
+                                         __builtin_elementwise_fma(f32x4{w0h, w0h, w0h, w0h}, tc[q][0], -fm));
         // branch-free: a hit lane re-requests its leading pair (an L1 hit next to the
-        // leading loads below) and selects the cached bytes; a divergent branch around
-        // the loads would make the waitcnt bookkeeping wait on the next quad's loads
-        // (the select happens at use, in unitc: here it would wait on the load at once)
+        // leading loads below), weighted 0; a divergent branch around the loads would make
+        // the waitcnt bookkeeping wait on the next quad's loads
         const int offT = (tc_hit ? obL : obT) * 16;
         Qm.t[0] = bld4(rf1, offT, po);
         Qm.t[1] = bld4(rf1, offT + 16, po);
-        Qm.t[2] = bld4(rf1, obL * 16, po);
-        Qm.t[3] = bld4(rf1, obL * 16 + 16, po);
+        tc[q][0] = bld4(rf1, obL * 16, po);  // the leading pair: this row's, and the next row's cache
+        tc[q][1] = bld4(rf1, obL * 16 + 16, po);
       };
 #pragma unroll
       for (int i = 0; i < RM - 1; ++i) issue_t(L[i], i);
@@ -1582,8 +1595,6 @@ __global__ __launch_bounds__(kThreads, 1) void ic_reduce_kernel(IterParams p) {
         f32x4* s0p = win + q * 64 + lane;          // slot 0
         f32x4* s1p = win + (NQW + q) * 64 + lane;  // slot 1
         const f32x4 wtop = *s0p, wmid = *s1p;      // rows above / at the pixel in marching order
-        const f32x4 tt0 = tc_hit ? tc[q][0] : cur.t[0];  // trailing pair (cached bytes on a hit)
-        const f32x4 tt1 = tc_hit ? tc[q][1] : cur.t[1];
 #pragma unroll
         for (int h = 0; h < 2; ++h) {  // channels 4q + 2h, 4q + 2h + 1
           auto half = [&](const f32x4& v) { return h ? f32x2{v.z, v.w} : f32x2{v.x, v.y}; };
@@ -1606,8 +1617,13 @@ __global__ __launch_bounds__(kThreads, 1) void ic_reduce_kernel(IterParams p) {
           const f32x2 n2 = x * x + (yv * yv + 1e-8f);
           const f32x2 inv = f32x2{__builtin_amdgcn_rsqf(n2.x), __builtin_amdgcn_rsqf(n2.y)};
           const f32x2 gx = x * inv, gy = yv * inv;
-          const f32x2 res = ((half(tt0) * wq.w0 - fm) + half(tt1) * wq.w1) + half(cur.t[2]) * wq.w2 +
-                            half(cur.t[3]) * wq.w3;
+          // ((T0 w0 - fm) + T1 w1) + t2 w2 + t3 w3 with T the trailing pair (cached on a hit):
+          // the hit and miss halves of each trailing term are exact (one factor is 0), so the
+          // sum is the one a select of T would give, bit for bit
+          const f32x2 rt = __builtin_elementwise_fma(f32x2{w1m, w1m}, half(cur.t[1]),
+                                                     __builtin_elementwise_fma(f32x2{w0m, w0m}, half(cur.t[0]), half(cur.P)));
+          const f32x2 res = __builtin_elementwise_fma(f32x2{wq.w3, wq.w3}, half(tc[q][1]),
+                                                      __builtin_elementwise_fma(f32x2{wq.w2, wq.w2}, half(tc[q][0]), rt));
           Q[0] += gx * gx;
           Q[1] += gx * gy;
           Q[2] += gy * gy;
@@ -1618,8 +1634,6 @@ __global__ __launch_bounds__(kThreads, 1) void ic_reduce_kernel(IterParams p) {
           Q[7] += gy;
           Q[8] += res;
         }
-        tc[q][0] = cur.t[2];  // the leading pair is the next row's trailing pair
-        tc[q][1] = cur.t[3];
         // straight-line code: the accumulators are pure arithmetic, which the DAG scheduler
         // would otherwise sink below every later load (all quads' loads first: 400 VGPRs)
         asm volatile("" : "+v"(Q[0]), "+v"(Q[1]), "+v"(Q[2]), "+v"(Q[3]), "+v"(Q[4]), "+v"(Q[5]), "+v"(Q[6]),
