@@ -313,12 +313,17 @@ struct Warp {
 // the CPU (geometry.py:63-85, 291-323): px = (u - cx) / fx; torch.bmm(R, [px,py,1])
 // = fma(R1, py, R0 * px) + R2 per row (measured bit-identical for every
 // shape used); + t * invD; u = (X / Z) * fx + cx; iz = invD / Z.
-__device__ __forceinline__ Warp warp_point(int x, int y, float d, const float* __restrict__ Rm,
-                                           const float* __restrict__ tv, float fx, float fy, float cx, float cy) {
+// the normalised pixel coordinates px = (u - cx) / fx, py = (v - cy) / fy
+__device__ __forceinline__ float norm_coord(int x, float c, float f) {
+#pragma clang fp contract(off)
+  return ((float)x - c) / f;
+}
+__device__ __forceinline__ Warp warp_point_n(float xr, float yr, float d, const float* __restrict__ Rm,
+                                             const float* __restrict__ tv, float fx, float fy, float cx, float cy) {
 #pragma clang fp contract(off)
   Warp w;
-  w.xr = ((float)x - cx) / fx;
-  w.yr = ((float)y - cy) / fy;
+  w.xr = xr;
+  w.yr = yr;
   const float X = (__builtin_fmaf(Rm[1], w.yr, Rm[0] * w.xr) + Rm[2]) + tv[0] * d;
   const float Y = (__builtin_fmaf(Rm[4], w.yr, Rm[3] * w.xr) + Rm[5]) + tv[1] * d;
   const float Z = (__builtin_fmaf(Rm[7], w.yr, Rm[6] * w.xr) + Rm[8]) + tv[2] * d;
@@ -326,6 +331,10 @@ __device__ __forceinline__ Warp warp_point(int x, int y, float d, const float* _
   w.v = (Y / Z) * fy + cy;
   w.iz = d / Z;
   return w;
+}
+__device__ __forceinline__ Warp warp_point(int x, int y, float d, const float* __restrict__ Rm,
+                                           const float* __restrict__ tv, float fx, float fy, float cx, float cy) {
+  return warp_point_n(norm_coord(x, cx, fx), norm_coord(y, cy, fy), d, Rm, tv, fx, fy, cx, cy);
 }
 
 // Last-block finalize parameters (one record per workgroup, fixed-order fp64 sums).
@@ -1175,7 +1184,8 @@ __global__ __launch_bounds__(kThreads, 1) void ic_reduce_kernel(IterParams p) {
     for (int r = 0; r < R; ++r) dv[r] = bld(rd0, min(y0 + r, H - 1) * W * 4 + min(max(xs, 0), W - 1) * 4, 0);
   };
   // frame of tile `it` from its inverse depths; issues the frame's gathers (consumed by pixel_terms)
-  auto make_frame_xy = [&](int xs, int y0, const float (&dv)[R], Frame& F, bool s0_rows) {
+  // xyr: the normalised coordinates of the pixel when the caller has them (R == 1), else null
+  auto make_frame_xy = [&](int xs, int y0, const float (&dv)[R], Frame& F, bool s0_rows, const float* xyr = nullptr) {
     F.y0 = y0;
     F.xc = min(max(xs, 0), W - 1);  // clamped: replicate padding of the stencil
     F.out_lane = (lane >= 1) && (lane <= kTileOut) && (xs < W);
@@ -1188,7 +1198,8 @@ __global__ __launch_bounds__(kThreads, 1) void ic_reduce_kernel(IterParams p) {
     for (int r = 0; r < R; ++r) {
       const int yr = min(F.y0 + r, H - 1);
       F.d[r] = dv[r];
-      F.wp[r] = warp_point(F.xc, yr, dv[r], Rm, tv, fx, fy, cx, cy);
+      F.wp[r] = xyr ? warp_point_n(xyr[0], xyr[1], dv[r], Rm, tv, fx, fy, cx, cy)
+                    : warp_point(F.xc, yr, dv[r], Rm, tv, fx, fy, cx, cy);
       F.tp[r] = make_taps(F.wp[r].u, F.wp[r].v, H, W);
       F.pw[r] = pair_weights(F.tp[r]);
       F.gd1[r] = gather4(rd1, F.tp[r], 0);
@@ -1417,43 +1428,52 @@ __global__ __launch_bounds__(kThreads, 1) void ic_reduce_kernel(IterParams p) {
     const float dirf = up ? -1.0f : 1.0f;
     // unit k of the wave's run -> (lane column xs, row y); strt: a strip begins at this
     // row in marching order (row H - 1 marching up, the strip's first row marching down)
-    auto unit_pos_st = [&](int k, int& xs, int& y, bool& strt) {
+    // run: units k, k + 1, ... up to k + run - 1 are rows y, y + dir, ... of the same strip
+    auto unit_pos_run = [&](int k, int& xs, int& y, bool& strt, int& run) {
       const int u = up ? uend - 1 - k : ubeg + k;
-      int strip, ytop = 0;
+      int strip, ytop = 0, ylo = 0, yhi = H;  // [ylo, yhi): the rows of this straight run's segment
       if (gpool) {
         const int m = gr1 - gr0;
         if (k < m) {  // own segment (k == 0 primes the window)
           strip = gs;
           y = up ? gr1 - 1 - k : gr0 + k;
           strt = false;
+          ylo = gr0;
+          yhi = gr1;
         } else {  // pool run: the left-over segments' units gpb .. gpe - 1, strip-major
           const int j = up ? gpe - 1 - (k - m) : gpb + (k - m);
           const int sp = j / gHL;
           strip = S_ - Eg + sp;
           y = gL0 + (j - sp * gHL);
           strt = k == m || y == (up ? H - 1 : gL0);
-        }
-        xs = strip * kTileOut - 1 + lane;
-        return;
-      }
-      if (hpool) {
-        const int uf = hnf * hLf;
-        if (u < uf) {
-          strip = u / max(hLf, 1);
-          y = hTf + (u - strip * hLf);
-          ytop = hTf;
-        } else {
-          const int s2 = (u - uf) / max(hLu, 1);
-          y = hTu + (u - uf - s2 * hLu);
-          strip = hnf + s2;
-          ytop = hTu;
+          ylo = gL0;
         }
       } else {
-        strip = u / H;
-        y = u - strip * H;
+        if (hpool) {
+          const int uf = hnf * hLf;
+          if (u < uf) {
+            strip = u / max(hLf, 1);
+            y = hTf + (u - strip * hLf);
+            ytop = hTf;
+          } else {
+            const int s2 = (u - uf) / max(hLu, 1);
+            y = hTu + (u - uf - s2 * hLu);
+            strip = hnf + s2;
+            ytop = hTu;
+          }
+        } else {
+          strip = u / H;
+          y = u - strip * H;
+        }
+        strt = y == (up ? H - 1 : ytop);
+        ylo = ytop;
       }
-      strt = y == (up ? H - 1 : ytop);
       xs = strip * kTileOut - 1 + lane;
+      run = min(up ? y - ylo + 1 : yhi - y, nrows - k);
+    };
+    auto unit_pos_st = [&](int k, int& xs, int& y, bool& strt) {
+      int run;
+      unit_pos_run(k, xs, y, strt, run);
     };
     auto unit_pos = [&](int k, int& xs, int& y) {
       bool strt;
@@ -1466,7 +1486,7 @@ __global__ __launch_bounds__(kThreads, 1) void ic_reduce_kernel(IterParams p) {
     struct QuadM {
       f32x4 f;      // f0 row y + dir
       f32x4 t[2];   // f1 trailing tap pair (on a tap-cache hit: a re-request of the leading pair)
-      f32x4 P;      // partial residual of the cached trailing pair (see issue_t)
+      f32x4 P;      // minus the partial residual of the cached trailing pair (see issue_t)
     };
     // Tap cache: in marching order, the f1 tap row a pixel row shares with
     // the next one is its LEADING row (lower row marching down, upper row marching up)
@@ -1497,10 +1517,28 @@ __global__ __launch_bounds__(kThreads, 1) void ic_reduce_kernel(IterParams p) {
     auto prefetch_f = [&](int i, int colq, int yn) {
       L[i].f = llvm_buf_load_f32x4(rf0, colq, i * 4 * (int)planeB + yn * W * 16, kF0Aux);
     };
+    // the current unit's position, carried from step to step: the next unit is the next row
+    // of the same strip while the straight run lasts (cu_run > 1), else (a few times per
+    // band) the full unit -> position mapping
+    int cu_xs = 0, cu_y = 0, cu_run = 0;
+    bool cu_st = false;
+    // Normalised coordinates without a division per row: px of the lane's column once per
+    // strip (at the window prime), py of 64 rows at a time (lane l: row ny_base + dir l),
+    // read back with one v_readlane per row -- the same IEEE divisions, fewer of them
+    float nx_lane = 0.f, ny_lanes = 0.f;
+    int ny_base = 0;
+    auto ny_refresh = [&](int yb) {
+      ny_base = yb;
+      ny_lanes = norm_coord(min(max(yb + dir * lane, 0), H - 1), cy, fy);
+    };
     if (nrows > 0) {
-      int xs0, y0;
-      unit_pos(0, xs0, y0);
+      unit_pos_run(0, cu_xs, cu_y, cu_st, cu_run);
+      cu_y = __builtin_amdgcn_readfirstlane(cu_y);
+      cu_run = __builtin_amdgcn_readfirstlane(cu_run);
+      cu_st = __builtin_amdgcn_readfirstlane((int)cu_st) != 0;
+      const int xs0 = cu_xs, y0 = cu_y;
       dnx = load_dpx(xs0, y0);
+      ny_refresh(y0);
 #pragma unroll
       for (int i = 0; i < RM - 1; ++i)
         if (kPf) prefetch_f(i, min(max(xs0, 0), W - 1) * 16, min(max(y0 + dir, 0), H - 1));
@@ -1510,13 +1548,13 @@ __global__ __launch_bounds__(kThreads, 1) void ic_reduce_kernel(IterParams p) {
     // The quad loop is straight-line with static quad indices (the tap cache lives in
     // registers), kRingQ quads in flight.
     auto step = [&](int k) {
-      int xs, y;
-      bool strt0;
-      unit_pos_st(k, xs, y, strt0);
+      const int xs = cu_xs, y = cu_y;
+      const bool strt0 = cu_st;
       const float dcur = dnx;
       const int colq = min(max(xs, 0), W - 1) * 16;
       if (k == 0 || strt0) {  // prime the window: rows y - dir (replicate-clamped) and y
         const int yp = min(max(y - dir, 0), H - 1);
+        nx_lane = norm_coord(min(max(xs, 0), W - 1), cx, fx);
 #pragma unroll
         for (int q = 0; q < NQW; ++q) {
           const int po = q * 4 * (int)planeB;
@@ -1543,13 +1581,31 @@ __global__ __launch_bounds__(kThreads, 1) void ic_reduce_kernel(IterParams p) {
       // the next step's (after the last step: this one's again, so that the loads are
       // unconditional -- a load under a branch makes the wait counts of every later quad
       // conservative)
-      int xs1, y1;
-      unit_pos(min(k + 1, nrows - 1), xs1, y1);
+      int xs1, y1, run1;
+      bool st1;
+      if (cu_run > 1) {
+        xs1 = xs;
+        y1 = y + dir;
+        st1 = false;
+        run1 = cu_run - 1;
+      } else {
+        unit_pos_run(min(k + 1, nrows - 1), xs1, y1, st1, run1);
+      }
+      // wave-uniform (a loop-carried value the uniformity analysis would otherwise lose)
+      cu_xs = xs1;
+      cu_y = y1 = __builtin_amdgcn_readfirstlane(y1);
+      cu_run = __builtin_amdgcn_readfirstlane(run1);
+      cu_st = __builtin_amdgcn_readfirstlane((int)st1) != 0;
       const int colq1 = min(max(xs1, 0), W - 1) * 16, yn1 = min(max(y1 + dir, 0), H - 1);
+      // py of this row: lane (y - ny_base) dir of the 64-row block (refreshed past its end or
+      // on a jump to another segment)
+      const int ny_off = (y - ny_base) * dir;
+      if (ny_off < 0 || ny_off >= 64) ny_refresh(y);
+      const float xyr[2] = {nx_lane, __int_as_float(__builtin_amdgcn_readlane(__float_as_int(ny_lanes), (y - ny_base) * dir))};
       Frame F;
       {
         const float dv[1] = {dcur};
-        make_frame_xy(xs, y, dv, F, false);
+        make_frame_xy(xs, y, dv, F, false, xyr);
       }
       // after the frame has consumed dcur: the new load then reuses its registers (a
       // loop-carried copy of a register with a load in flight would wait for every load)
@@ -1574,9 +1630,11 @@ __global__ __launch_bounds__(kThreads, 1) void ic_reduce_kernel(IterParams p) {
         // is loaded into its registers (no copy of the cache per row):
         // P = w1h tc1 + (w0h tc0 - fm), fm = f0 row y from the window -- the first two terms
         // of the residual, in the order the residual sums them (below).  On a miss P = -fm.
+        // (stored negated, -P = fm - w0h tc0 - w1h tc1 exactly: the negation then folds into the
+        // consuming fma as a source modifier instead of a v_xor per element)
         const f32x4 fm = win[(NQW + q) * 64 + lane];
-        Qm.P = __builtin_elementwise_fma(f32x4{w1h, w1h, w1h, w1h}, tc[q][1],
-                                         __builtin_elementwise_fma(f32x4{w0h, w0h, w0h, w0h}, tc[q][0], -fm));
+        Qm.P = __builtin_elementwise_fma(f32x4{-w1h, -w1h, -w1h, -w1h}, tc[q][1],
+                                         __builtin_elementwise_fma(f32x4{-w0h, -w0h, -w0h, -w0h}, tc[q][0], fm));
         // branch-free: a hit lane re-requests its leading pair (an L1 hit next to the
         // leading loads below), weighted 0; a divergent branch around the loads would make
         // the waitcnt bookkeeping wait on the next quad's loads
@@ -1621,7 +1679,7 @@ __global__ __launch_bounds__(kThreads, 1) void ic_reduce_kernel(IterParams p) {
           // the hit and miss halves of each trailing term are exact (one factor is 0), so the
           // sum is the one a select of T would give, bit for bit
           const f32x2 rt = __builtin_elementwise_fma(f32x2{w1m, w1m}, half(cur.t[1]),
-                                                     __builtin_elementwise_fma(f32x2{w0m, w0m}, half(cur.t[0]), half(cur.P)));
+                                                     __builtin_elementwise_fma(f32x2{w0m, w0m}, half(cur.t[0]), -half(cur.P)));
           const f32x2 res = __builtin_elementwise_fma(f32x2{wq.w3, wq.w3}, half(tc[q][1]),
                                                       __builtin_elementwise_fma(f32x2{wq.w2, wq.w2}, half(tc[q][0]), rt));
           Q[0] += gx * gx;
