@@ -1471,14 +1471,6 @@ __global__ __launch_bounds__(kThreads, 1) void ic_reduce_kernel(IterParams p) {
       xs = strip * kTileOut - 1 + lane;
       run = min(up ? y - ylo + 1 : yhi - y, nrows - k);
     };
-    auto unit_pos_st = [&](int k, int& xs, int& y, bool& strt) {
-      int run;
-      unit_pos_run(k, xs, y, strt, run);
-    };
-    auto unit_pos = [&](int k, int& xs, int& y) {
-      bool strt;
-      unit_pos_st(k, xs, y, strt);
-    };
     // window in LDS, per wave [2 slots][NQ quads][64 lanes] (each lane only ever touches
     // its own column and a wave's LDS accesses complete in order: no barrier)
     f32x4* win = lds_win[wave];
