@@ -50,6 +50,12 @@ def parse():
                    help="pairs per independent batch (one reference call: its own batch-global extrema)")
     p.add_argument("--inflight", type=int, default=4,
                    help="consecutive steps of the stream in flight per GPU (one stream, graph, workspace each)")
+    p.add_argument("--stream-group", type=int, default=0,
+                   help="global batches of the stream per grouped call on each rank (0: enough for "
+                        "--min-launch-pairs pairs per call)")
+    p.add_argument("--min-launch-pairs", type=int, default=64,
+                   help="stream grouping target: pairs per call and rank (the N = 1 launch holds the whole "
+                        "64-pair global batch)")
     p.add_argument("--icp", action="store_true", help="cfg5: with the combine_ICP term (weight 0.01)")
     p.add_argument("--setup-warm-ms", type=float, default=200.0,
                    help="setup: replay solves for this long before the --warmup steps (the GPU clock ramps over "
@@ -290,35 +296,48 @@ def main():
     if weak:
         n_r = a.pairs_per_gpu
         per_step = world * n_r
-        first = lambda j: (rank * S + j) * max(1, n_r // a.batch)
+        begin = 0
+        step_first = lambda k: (rank * 1_000_000 + k) * max(1, n_r // a.batch)  # this rank's own stream
     else:
         per_step = a.global_batch
         begin, end = shard.shard_range(per_step, world, rank)
         n_r = end - begin
         if n_r < 1:
             raise SystemExit(f"global batch {per_step} < {world} ranks")
-        first = lambda j: j * max(1, per_step // a.batch) + begin // a.batch
+        step_first = lambda k: k * max(1, per_step // a.batch) + begin // a.batch  # global batch k's shard
     B = a.batch if n_r % a.batch == 0 and (weak or begin % a.batch == 0) else n_r
-    G = n_r // B  # independent batches per call (DPFT_GROUP)
-    slot_inputs = [make_batches(B, first(j), G, device, a.icp) for j in range(S)]
+    G = n_r // B  # independent batches per step (DPFT_GROUP)
+    # stream grouping: a rank solves Q consecutive global batches of the stream in ONE grouped
+    # call (each batch still its own reference call), so that a call holds >= --min-launch-pairs
+    # pairs whatever the shard size -- the N = 8 rank load (8 pairs per global batch) then runs
+    # the same 64-pair launches as N = 1 instead of 8-pair launches
+    Q = a.stream_group if a.stream_group > 0 else shard.stream_group(n_r, B, a.min_launch_pairs)
+    calls_for = lambda steps: shard.stream_calls(steps, Q)
+
+    def inputs_for(call_idx, q):
+        """Inputs of call `call_idx` (q global batches: steps call_idx * Q .. + q - 1)."""
+        parts = [make_batches(B, step_first(call_idx * Q + k), G, device, a.icp) for k in range(q)]
+        if q == 1:
+            return parts[0]
+        return (sum((p_[0] for p_ in parts), []),
+                [{k: torch.cat([p_[1][l][k] for p_ in parts]) for k in parts[0][1][l]} for l in range(LEVELS)],
+                torch.cat([p_[2] for p_ in parts]))
+    slot_inputs = [inputs_for(j, Q) for j in range(S)]
     sel, levels_nchw, K = slot_inputs[0]
 
     def packed(levels):
         return [dict(d, x0=ic.pack_features(d["x0"]), x1=ic.pack_features(d["x1"])) for d in levels]
-
-    pose_init = torch.cat((torch.eye(3, device=device).repeat(n_r, 1, 1).reshape(-1),
-                           torch.zeros(n_r * 3, device=device)))
 
     def capture(fn):
         fn()
         torch.cuda.synchronize()
         if a.no_graph:
             return fn
-        s = torch.cuda.Stream(device)
-        s.wait_stream(torch.cuda.current_stream(device))
-        with torch.cuda.stream(s):
+        s_ = torch.cuda.Stream(device)
+        s_.wait_stream(torch.cuda.current_stream(device))
+        with torch.cuda.stream(s_):
             fn()
-        torch.cuda.current_stream(device).wait_stream(s)
+        torch.cuda.current_stream(device).wait_stream(s_)
         graph = torch.cuda.CUDAGraph()
         with torch.cuda.graph(graph):
             fn()
@@ -326,10 +345,14 @@ def main():
         return graph.replay
 
     def make_step(levels, K, pre=None):
+        """A call's solver, pose buffers and graph-captured solve (every pair from identity)."""
+        n = K.shape[0]
+        pose_init = torch.cat((torch.eye(3, device=device).repeat(n, 1, 1).reshape(-1),
+                               torch.zeros(n * 3, device=device)))
         solver = ic.PyramidSolver(levels, K, iters=ITERS, remove_tru_sigma=True, combine_icp=a.icp,
-                                  group=B if G > 1 else None)
+                                  group=B if n > B else None)
         pose = pose_init.clone()
-        R, t = pose[:9 * n_r].view(n_r, 3, 3), pose[9 * n_r:].view(n_r, 3)
+        R, t = pose[:9 * n].view(n, 3, 3), pose[9 * n:].view(n, 3)
 
         def solve():
             if pre is not None:
@@ -339,13 +362,21 @@ def main():
         solve()
         torch.cuda.synchronize()
         ic.check_status(solver.status)
+        solver.bench_keep = (pose_init, pose, pre)  # a captured graph reads them (pre: its buffers): keep alive
         return solver, R, t, capture(solve)
 
     slot_levels = [packed(si[1]) if a.layout == "c4" else si[1] for si in slot_inputs]
     slots = [make_step(slot_levels[j], slot_inputs[j][2]) for j in range(S)]
+    # a short last call (K or W not a multiple of Q): q < Q global batches, its own graph
+    rems = sorted({c for c in calls_for(a.steps) + calls_for(a.warmup) if c != Q})
+    rem_slots, rem_inputs, rem_levels = {}, {}, {}
+    for q in rems:
+        rem_inputs[q] = ri = inputs_for(S, q)
+        rem_levels[q] = packed(ri[1]) if a.layout == "c4" else ri[1]
+        rem_slots[q] = make_step(rem_levels[q], ri[2])
     streams = [torch.cuda.Stream(device) for _ in range(S)]
     solver, R, t, run = slots[0]
-    gathered = [torch.empty(world * n_r, 12, device=device) for _ in range(2)] if world > 1 else None
+    gathered = {}
     pending = [None]
 
     def drain():
@@ -358,20 +389,24 @@ def main():
             import torch.distributed as dist
             dist.barrier()
 
-    def timed_loop(slots, steps, warmup):
-        """W warm-up then K timed steps (step k on slot k % S), barrier + synchronize on both
-        sides; the N > 1 pose gather of step k overlaps step k + 1 (double-buffered)."""
-        nstep = [0]
+    def timed_loop(slots, rem_slots, steps, warmup):
+        """W warm-up then K timed global batches (call c on slot c % S, Q batches per call, a
+        remainder call where Q does not divide), barrier + synchronize on both sides; the
+        N > 1 pose gather of call c overlaps call c + 1 (double-buffered)."""
+        ncall = [0]
 
-        def step():
-            j = nstep[0] % len(slots)
+        def call(q):
+            j = ncall[0] % len(slots)
+            sl = slots[j] if q == Q else rem_slots[q]
             with torch.cuda.stream(streams[j]):
-                slots[j][3]()
+                sl[3]()
                 if world > 1:
                     drain()
-                    _, pending[0] = shard.gather_poses(slots[j][1], slots[j][2], out=gathered[nstep[0] % 2],
-                                                       async_op=True)
-            nstep[0] += 1
+                    key = (q, ncall[0] % 2)
+                    if key not in gathered:
+                        gathered[key] = torch.empty(world * q * n_r, 12, device=device)
+                    _, pending[0] = shard.gather_poses(sl[1], sl[2], out=gathered[key], async_op=True)
+            ncall[0] += 1
         # setup warm-up by wall time, solves only (no collective: ranks run different counts)
         torch.cuda.synchronize()
         tw = time.perf_counter()
@@ -380,15 +415,15 @@ def main():
                 with torch.cuda.stream(streams[j]):
                     sl[3]()
             torch.cuda.synchronize()
-        for _ in range(warmup):
-            step()
+        for q in calls_for(warmup):
+            call(q)
         drain()
         torch.cuda.synchronize()
         barrier()
         torch.cuda.synchronize()
         t0 = time.perf_counter()
-        for _ in range(steps):
-            step()
+        for q in calls_for(steps):
+            call(q)
         drain()
         torch.cuda.synchronize()
         barrier()
@@ -401,38 +436,65 @@ def main():
             el = e.item()
         return el
 
-    log(f"rank {rank}: {n_r} pairs per step in {G} batch(es) of {B}, {S} in flight; timing {a.steps} steps")
-    elapsed = timed_loop(slots, a.steps, a.warmup)
-    log(f"rank {rank}: {elapsed / a.steps * 1e3:.3f} ms per step")
-    for sl in slots:
+    log(f"rank {rank}: {n_r} pairs per global batch in {G} batch(es) of {B}; {Q} global batch(es) per call, "
+        f"{S} calls in flight; timing {a.steps} global batches")
+    elapsed = timed_loop(slots, rem_slots, a.steps, a.warmup)
+    log(f"rank {rank}: {elapsed / a.steps * 1e3:.3f} ms per global batch")
+    for sl in slots + list(rem_slots.values()):
         ic.check_status(sl[0].status)
     ms_per_step = elapsed / a.steps * 1e3
     value = per_step * LEVELS * ITERS * a.steps / elapsed
+    n_call = n_r * Q  # pairs per call (launch) on this rank
 
-    # end-to-end from the reference's NCHW layout: the step also packs both frames' feature
-    # pyramids into the channel-quad buffers the solve reads (every pair packs its own two
-    # frames), captured in the same graph; same timed loop (rank 0 and all ranks alike)
+    # Encoder-to-solve: each call also runs the feature heads' epilogue (batchnorm + ELU of the
+    # f_conv heads, algorithms.py:1273-1277) of both frames' 4 levels for every pair, which the
+    # drop-in's encoder stores straight in the solver's channel-quad layout (dpft_bn_elu_pack)
+    # -- the heads' conv outputs stand in as the NCHW features in channels_last with the
+    # identity batchnorm (a = 1, b = 0: the features are >= 0, so ELU leaves them unchanged and
+    # the solve sees the headline's inputs); and for comparison the previous route, the
+    # in-place epilogue (dpft_bn_elu) followed by the relayout (dpft_pack_features_nhwc)
     e2e = None
     if a.layout == "c4" and not a.no_compare:
-        def packer(src, dst):
-            L = ic.N.lib()
+        Lb = ic.N.lib()
+        chan = torch.cat((torch.ones(C, device=device), torch.zeros(C, device=device))).contiguous()
 
-            def pk():
+        def epilogue(src, dst, fused):
+            conv = [{k: d[k].contiguous(memory_format=torch.channels_last) for k in ("x0", "x1")} for d in src]
+            work = [{k: torch.empty_like(c[k]) for k in c} for c in conv] if not fused else None
+
+            def run_epilogue():
                 for l in range(LEVELS):
                     for key in ("x0", "x1"):
-                        s_, d_ = src[l][key], dst[l][key]
-                        ic.N.check(L.dpft_pack_features(ic._ptr(s_), ic._ptr(d_), s_.shape[0], C, s_.shape[2],
-                                                        s_.shape[3], ic._stream(device)), "dpft_pack_features")
-            return pk
-        e2e_slots = [make_step(slot_levels[j], slot_inputs[j][2], pre=packer(slot_inputs[j][1], slot_levels[j]))
-                     for j in range(S)]
-        el = timed_loop(e2e_slots, a.steps, a.warmup)
-        e2e = {"value": per_step * LEVELS * ITERS * a.steps / el, "ms_per_step": el / a.steps * 1e3,
-               "what": "each step also converts both frames' NCHW feature pyramids (x0, x1, 4 levels, every pair) "
-                       "to the channel-quad layout (dpft_pack_features) inside the timed graph"}
-        del e2e_slots
-
-    # latency of one step alone (slot 0, back to back on one stream), rank 0 only
+                        c_, d_ = conv[l][key], dst[l][key]
+                        Bn, Cn, Hn, Wn = c_.shape
+                        if fused:
+                            ic.N.check(Lb.dpft_bn_elu_pack(ic._ptr(c_), ic._ptr(chan), ic._ptr(d_), Bn, Cn, Hn, Wn,
+                                                           ic._stream(device)), "dpft_bn_elu_pack")
+                        else:
+                            w_ = work[l][key]
+                            w_.copy_(c_)
+                            ic.N.check(Lb.dpft_bn_elu(ic._ptr(w_), ic._ptr(chan), w_.numel(), Cn, 1, 1,
+                                                      ic._stream(device)), "dpft_bn_elu")
+                            ic.N.check(Lb.dpft_pack_features_nhwc(ic._ptr(w_), ic._ptr(d_), Bn, Cn, Hn, Wn,
+                                                                  ic._stream(device)), "dpft_pack_features_nhwc")
+            return run_epilogue
+        e2e = {}
+        for tag, fused in (("fused_epilogue", True), ("epilogue_then_relayout", False)):
+            e_slots = [make_step(slot_levels[j], slot_inputs[j][2], pre=epilogue(slot_inputs[j][1], slot_levels[j],
+                                                                                  fused)) for j in range(S)]
+            e_rem = {q: make_step(rem_levels[q], rem_inputs[q][2], pre=epilogue(rem_inputs[q][1], rem_levels[q], fused))
+                     for q in rem_slots}
+            el = timed_loop(e_slots, e_rem, a.steps, a.warmup)
+            same = all(torch.equal(es[1], sl[1]) and torch.equal(es[2], sl[2]) for es, sl in zip(e_slots, slots))
+            e2e[tag] = {"value": per_step * LEVELS * ITERS * a.steps / el, "ms_per_step": el / a.steps * 1e3,
+                        "frac_of_headline": (per_step * LEVELS * ITERS * a.steps / el) / value,
+                        "poses_equal_headline": same}
+            del e_slots, e_rem
+        e2e["what"] = ("each call also runs the feature heads' batchnorm + ELU epilogue of both frames' 4-level "
+                       "feature maps of every pair (conv outputs resident in HBM, channels_last): 'fused_epilogue' "
+                       "stores the solver's channel-quad layout directly (dpft_bn_elu_pack, the drop-in's encoder); "
+                       "'epilogue_then_relayout' = in-place epilogue + dpft_pack_features_nhwc (the previous drop-in)")
+    # latency of one call alone (slot 0, back to back on one stream), rank 0 only
     latency_ms = None
     if rank == 0:
         n_lat = min(a.steps, 50)
@@ -457,7 +519,7 @@ def main():
     achieved = alg_bytes / (kern_us * 1e-6) / 1e9
     mode = 1 if a.icp else 0
     kname = f"_ZN12_GLOBAL__N_116ic_reduce_kernelILi32ELb1ELb1ELi{mode}ELb1EEEvNS_10IterParamsE"
-    traffic = l0_traffic(n_r, B, kname) if a.layout == "c4" else None
+    traffic = l0_traffic(n_call, B, kname) if a.layout == "c4" else None
     copy_gbs = copy_peak_gbs(device) if rank == 0 else None
     read_gbs = read_peak_gbs(device, alg_bytes) if rank == 0 else None
 
@@ -469,7 +531,7 @@ def main():
             o_run()
         sec = _timed(o_run, a.steps, device)
         other = {"layout": other_layout, "ms_per_step_sequential": sec * 1e3,
-                 "value_sequential": n_r * LEVELS * ITERS / sec,
+                 "value_sequential": n_call * LEVELS * ITERS / sec,
                  "max_abs_pose_diff_vs_headline": max((o_R - R).abs().max().item(), (o_t - t).abs().max().item())}
         del o_solver
 
@@ -493,12 +555,13 @@ def main():
                                     "weak scaling, %d pairs per GPU per step, " % n_r) +
                                    "640x480, C=32, Cs=1, 4 levels x 3 GN iters, remove_tru_sigma" +
                                    (", combine_ICP (w=0.01)" if a.icp else ""),
-                       "global_batch": per_step, "pairs_per_gpu": n_r, "batch": B, "batches_per_launch": G,
-                       "pairs_per_launch": n_r, "inflight": S,
+                       "global_batch": per_step, "pairs_per_gpu": n_r, "batch": B,
+                       "stream_group": Q, "batches_per_launch": G * Q, "pairs_per_launch": n_call, "inflight": S,
                        "parallelism": f"pair-sharded x{world}, RCCL all-gather of poses",
                        "graph": not a.no_graph, "feature_layout": a.layout, "setup_warm_ms": a.setup_warm_ms},
             "latency_ms_per_step": latency_ms,
-            "latency_what": f"one step alone on rank 0: its {n_r} pairs, 4 levels x 3 iterations, nothing else in flight",
+            "latency_what": f"one call alone on rank 0: its {n_call} pairs ({Q} global batch(es)), 4 levels x 3 "
+                            f"iterations, nothing else in flight",
             "pairs_per_s": per_step * a.steps / elapsed,
             "l0_iters_per_s": per_step * ITERS * a.steps / elapsed,
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
@@ -506,14 +569,14 @@ def main():
                          "traffic": traffic["hbm_bytes"] if traffic else None,
                          "traffic_source": traffic["source"] if traffic else None,
                          "kernel": f"ic_reduce_kernel<32,Cs=1,tru,{'U_IC+ICP' if a.icp else 'U_IC'},{a.layout}> "
-                                   f"(level 0, {n_r} pairs per launch, + in-kernel finalize)",
+                                   f"(level 0, {n_call} pairs per launch, + in-kernel finalize)",
                          "kernel_us": kern_us, "algorithmic_bytes_per_launch": alg_bytes,
                          "algorithmic_bytes_per_pixel": bpa,
                          "measured_copy_peak": copy_gbs,
                          "frac_of_measured_copy_peak": achieved / copy_gbs if copy_gbs else None,
                          "measured_read_peak": read_gbs,
                          "frac_of_measured_read_peak": achieved / read_gbs if read_gbs else None},
-            "end_to_end_from_nchw": e2e,
+            "encoder_epilogue_to_solve": e2e,
             "cpu_baseline": cpu,
             "other_layout": other,
         }

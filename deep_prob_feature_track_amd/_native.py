@@ -48,7 +48,7 @@ class LevelTensors(ctypes.Structure):
 EXPORTS = ("dpft_workspace_size", "dpft_ic_solve_level", "dpft_ic_solve_pyramid", "dpft_ic_iterate", "dpft_ic_residual_level",
            "dpft_residual_poses_workspace_size", "dpft_ic_residual_poses", "dpft_ic_residual_map",
            "dpft_ic_reduce_only", "dpft_ic_debug_pixels", "dpft_preprocess_workspace_size",
-           "dpft_preprocess_depth", "dpft_pack_features", "dpft_pack_features_nhwc", "dpft_bn_elu", "dpft_sigma_extrema_levels", "dpft_ic_damped_update", "dpft_feature_gradient", "dpft_warp_jacobian",
+           "dpft_preprocess_depth", "dpft_pack_features", "dpft_pack_features_nhwc", "dpft_bn_elu", "dpft_bn_elu_pack", "dpft_sigma_extrema_levels", "dpft_ic_damped_update", "dpft_feature_gradient", "dpft_warp_jacobian",
            "dpft_inverse_jacobian", "dpft_normal_equations_workspace_size", "dpft_normal_equations",
            "dpft_read_probe_out_floats", "dpft_read_probe", "dpft_copy_probe", "dpft_version", "dpft_last_error")
 
@@ -98,6 +98,8 @@ def lib():
     L.dpft_pack_features_nhwc.restype = ctypes.c_int
     L.dpft_bn_elu.argtypes = [vp, vp, ctypes.c_int64, ctypes.c_int32, ctypes.c_int64, ctypes.c_int32, vp]
     L.dpft_bn_elu.restype = ctypes.c_int
+    L.dpft_bn_elu_pack.argtypes = [vp, vp, vp, ctypes.c_int32, ctypes.c_int32, ctypes.c_int32, ctypes.c_int32, vp]
+    L.dpft_bn_elu_pack.restype = ctypes.c_int
     L.dpft_ic_damped_update.argtypes = [vp, vp, vp, ctypes.c_int32, ctypes.c_int32, vp, vp, vp, vp, vp]
     L.dpft_ic_damped_update.restype = ctypes.c_int
     i32 = ctypes.c_int32

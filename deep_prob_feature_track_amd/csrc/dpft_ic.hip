@@ -624,20 +624,26 @@ __device__ __forceinline__ IcpTerm icp_pixel(float xr, float yr, float d0, const
   const float n0 = __builtin_fmaf(Nz, Rm[6], __builtin_fmaf(Ny, Rm[3], Nx * Rm[0]));
   const float n1 = __builtin_fmaf(Nz, Rm[7], __builtin_fmaf(Ny, Rm[4], Nx * Rm[1]));
   const float n2 = __builtin_fmaf(Nz, Rm[8], __builtin_fmaf(Ny, Rm[5], Nx * Rm[2]));
-  // stereo-model sigma with the reference's hard-coded TUM constants (975-997)
-  const float sxy = d0 / 525.0f * 5.5f;
-  const float sz = d0 * d0 * 0.4f / (525.0f * 1.2f);
+  // stereo-model sigma with the reference's hard-coded TUM constants (975-997).  Only the
+  // divisions above feed discrete tests (the in-view test and the taps: X / Z, Y / Z; the
+  // ||diff|| > 0.1 occlusion: the tap vertices) and stay op for op.  These only scale
+  // continuous values: the constants are folded (depth / 525 * 5.5 -> depth * (5.5 / 525),
+  // depth^2 * 0.4 / (525 * 1.2) -> depth^2 * (0.4 / 630)) and the seven divisions by
+  // sigma_icp + 1e-8 (965-966) are one reciprocal and seven products (each within an ulp
+  // of the quotient; the JtJ / JtR bounds are 1e-5 / 1e-4 relative)
+  constexpr float kSxy = 5.5f / 525.0f, kSz = 0.4f / (525.0f * 1.2f);
+  const float sxy = d0 * kSxy;
+  const float sz = (d0 * d0) * kSz;
   const float cov = (((n0 * sxy) * sxy) * n0 + ((n1 * sxy) * sxy) * n1) + ((n2 * sz) * sz) * n2;
-  const float sig = sqrtf(cov + 1e-8f) + 1e-8f;
+  const float rsig = wgt / (sqrtf(cov + 1e-8f) + 1e-8f);  // w / sigma: the ScaleNet weight folded in
   IcpTerm o;
-  o.J[0] = -((n1 * V0z - n2 * V0y) / sig) * wgt;
-  o.J[1] = -((n2 * V0x - n0 * V0z) / sig) * wgt;
-  o.J[2] = -((n0 * V0y - n1 * V0x) / sig) * wgt;
-  o.J[3] = -((-n0) / sig) * wgt;
-  o.J[4] = -((-n1) / sig) * wgt;
-  o.J[5] = -((-n2) / sig) * wgt;
-  r = r / sig;
-  o.r = (occ ? 1e-6f : r) * wgt;
+  o.J[0] = (n2 * V0y - n1 * V0z) * rsig;
+  o.J[1] = (n0 * V0z - n2 * V0x) * rsig;
+  o.J[2] = (n1 * V0x - n0 * V0y) * rsig;
+  o.J[3] = n0 * rsig;
+  o.J[4] = n1 * rsig;
+  o.J[5] = n2 * rsig;
+  o.r = occ ? 1e-6f * wgt : r * rsig;
   o.occ = occ;
   return o;
 }
@@ -3514,6 +3520,26 @@ __global__ __launch_bounds__(kThreads) void bn_elu_kernel(f32x4* __restrict__ x,
   }
   x[i] = v;
 }
+
+// dpft_bn_elu_pack: bn_elu_kernel<true>'s epilogue on a channels_last conv output, stored to
+// the channel-quad layout with pack_c4_nhwc_kernel's mapping (thread r of pair row b =
+// blockIdx.y reads quad r of the pair's [HW][C] block; 64 lanes = 64 / Q pixels x Q planes,
+// one 128-byte run per plane at Q = 8).  The conv output is read once (non-temporal).
+__global__ __launch_bounds__(kThreads) void bn_elu_pack_kernel(const f32x4* __restrict__ src,
+                                                               const float* __restrict__ chan,
+                                                               f32x4* __restrict__ dst, uint32_t n, uint32_t Q,
+                                                               uint32_t HW) {
+  const uint32_t r = blockIdx.x * kThreads + threadIdx.x;
+  if (r >= n) return;
+  const size_t base = (size_t)blockIdx.y * n;
+  const uint32_t pix = r / Q, q = r - pix * Q, C = 4 * Q, c = 4 * q;
+  f32x4 v = __builtin_nontemporal_load(src + base + r);
+  v.x = bn_elu1(v.x, chan, C, c);
+  v.y = bn_elu1(v.y, chan, C, c + 1);
+  v.z = bn_elu1(v.z, chan, C, c + 2);
+  v.w = bn_elu1(v.w, chan, C, c + 3);
+  dst[base + (size_t)q * HW + pix] = v;
+}
 }  // namespace
 
 extern "C" {
@@ -3678,6 +3704,20 @@ int dpft_bn_elu(float* x, const float* chan, int64_t n, int32_t C, int64_t inner
     hipLaunchKernelGGL(bn_elu_kernel<false>, grid, dim3(kThreads), 0, st, x4, chan, n4, (uint32_t)C,
                        (uint32_t)(inner / 4));
   return hip_check("bn_elu_kernel");
+}
+
+int dpft_bn_elu_pack(const float* x, const float* chan, float* out, int32_t B, int32_t C, int32_t H, int32_t W,
+                     void* hip_stream) {
+  if (!x || !chan || !out || x == out) return fail(DPFT_E_INVALID, "null or aliased pointer");
+  if (B < 1 || B > 65535 || C < 4 || C % 4 != 0 || H < 1 || W < 1 || (long)H * W * (C / 4) >= (1L << 31))
+    return fail(DPFT_E_INVALID, "bad shape B=%d C=%d H=%d W=%d (C %% 4 == 0 needed)", B, C, H, W);
+  if ((reinterpret_cast<uintptr_t>(x) | reinterpret_cast<uintptr_t>(out)) & 15)
+    return fail(DPFT_E_INVALID, "x / out must be 16-byte aligned");
+  const uint32_t Q = (uint32_t)(C / 4), HW = (uint32_t)H * (uint32_t)W, n = HW * Q;
+  hipLaunchKernelGGL(bn_elu_pack_kernel, dim3((n + kThreads - 1) / kThreads, (unsigned)B), dim3(kThreads), 0,
+                     static_cast<hipStream_t>(hip_stream), reinterpret_cast<const f32x4*>(x), chan,
+                     reinterpret_cast<f32x4*>(out), n, Q, HW);
+  return hip_check("bn_elu_pack_kernel");
 }
 
 int dpft_version(void) { return DPFT_ABI_VERSION; }

@@ -14,15 +14,14 @@ pair order; rank 0 writes the reference's pkl / CSV (metrics.write_results).
     python -m torch.distributed.run --nproc-per-node N --master-addr 127.0.0.1 \\
         -m deep_prob_feature_track_amd.evaluate --pairs 64 --batch 8 --out eval_out
 
-The CLI evaluates the TUM fr1/desk example frames the reference ships (stored in
-tests/golden/tum_fr1_desk_frames.npz; the datasets and checkpoints are absent): the
-ordered pairs cycled to --pairs, the tracker with its deterministic synthetic weights
-(tests/golden/recipe.py), ground truth = identity (no poses ship with the frames), so the
+The CLI evaluates the TUM fr1/desk example frames the reference ships (examples.py:
+data/tum_fr1_desk_frames.npz; the datasets and checkpoints are absent): the ordered pairs
+cycled to --pairs, the tracker with deterministic synthetic weights
+(examples.synthetic_weights), ground truth = identity (no poses ship with the frames), so the
 errors are the estimated motions' magnitudes.
 """
 import argparse
 import os
-import sys
 
 import numpy as np
 import torch
@@ -77,18 +76,16 @@ def rows_to_outputs(rows, names):
 def _example_loader(n_pairs, H, W, device):
     """TUM fr1/desk example pairs (ordered pairs of the five frames, cycled), ground truth
     identity; color [3,H,W] in [0,1], depth in m clipped to [0.5, 5] (SimpleLoader.py:77-80)."""
-    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-    sys.path.insert(0, os.path.join(root, "tests", "golden"))
-    import recipe
+    from . import examples as ex
     down = 640 // W
-    pairs = [recipe.ORDERED_PAIRS[k % len(recipe.ORDERED_PAIRS)] for k in range(n_pairs)]
+    pairs = [ex.ORDERED_PAIRS[k % len(ex.ORDERED_PAIRS)] for k in range(n_pairs)]
 
     def load(i0, i1):
         sel = pairs[i0:i1]
         b = len(sel)
-        col = lambda i: torch.from_numpy(recipe.color_float(i, down))
-        dep = lambda i: torch.from_numpy(recipe.depth_m(i, down))[None]
-        K = torch.from_numpy(np.tile(recipe.K_FULL[None] / down, (b, 1)))
+        col = lambda i: torch.from_numpy(ex.color_float(i, down))
+        dep = lambda i: torch.from_numpy(ex.depth_m(i, down))[None]
+        K = torch.from_numpy(np.tile(ex.K_FULL[None] / down, (b, 1)))
         return {"color0": torch.stack([col(i) for i, _ in sel]).to(device),
                 "color1": torch.stack([col(j) for _, j in sel]).to(device),
                 "depth0": torch.stack([dep(i) for i, _ in sel]).to(device),
@@ -99,18 +96,13 @@ def _example_loader(n_pairs, H, W, device):
 
 def _tracker(C, device):
     """The drop-in LeastSquareTracking (ConvRGBD2 encoder, laplacian uncertainty, U_IC,
-    remove_tru_sigma) with the recipe's deterministic synthetic weights."""
-    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-    sys.path.insert(0, os.path.join(root, "tests", "golden"))
-    import recipe
+    remove_tru_sigma) with deterministic synthetic weights (examples.py)."""
+    from .examples import load_synthetic_weights
     from .models.LeastSquareTracking import LeastSquareTracking, default_options
     net = LeastSquareTracking("ConvRGBD2", "laplacian", 3, "None", "Direct-Nodamping",
                               options=default_options(feature_channel=C, uncertainty_channel=1,
                                                       feature_extract="conv", remove_tru_sigma=True))
-    sd = {k: torch.from_numpy(np.asarray(recipe.synthetic_weights(k, v.shape))).to(v.dtype)
-          for k, v in net.state_dict().items()}
-    net.load_state_dict(sd)
-    return net.to(device).eval()
+    return load_synthetic_weights(net).to(device).eval()
 
 
 def main():

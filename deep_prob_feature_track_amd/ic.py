@@ -129,12 +129,48 @@ def bn_elu_(x, bn):
         nhwc, inner, ok = 0, H * W, (H * W) % 4 == 0
     else:
         return False
-    if not ok or x.data_ptr() % 16 or C != bn.num_features:
+    if not ok or C != bn.num_features:
         return False
     chan = _bn_coeffs(bn, x.device)
+    if x.data_ptr() % 16:  # the kernel's 16-byte accesses (conv outputs are allocator-aligned)
+        bn_elu_unaligned_(x, chan)
+        return True
     rc = N.lib().dpft_bn_elu(_ptr(x), _ptr(chan), x.numel(), C, inner, nhwc, _stream(x.device))
     N.check(rc, "dpft_bn_elu")
     return True
+
+
+def bn_elu_pack_applies(x, bn):
+    """The conv outputs dpft_bn_elu_pack takes: an fp32 channels_last map with C % 4 == 0 on
+    the device, an eval-mode BatchNorm2d with running statistics (traceable: shapes,
+    strides, dtype only; alignment is checked at the call)."""
+    return (x.is_cuda and x.dtype == torch.float32 and x.dim() == 4 and bn.running_mean is not None
+            and x.shape[1] == bn.num_features and x.shape[1] % 4 == 0 and channels_last(x))
+
+
+@_eager_only
+def bn_elu_pack(x, bn):
+    """ELU(bn(x)) of a channels_last conv output, written to the channel-quad layout
+    [B,C/4,H,W,4] the solver reads (dpft_bn_elu_pack): the feature heads' epilogue
+    (algorithms.py:1273-1277) and the relayout in one pass.  The values are those of
+    bn_elu_ + pack_features."""
+    B, C, H, W = x.shape
+    chan = _bn_coeffs(bn, x.device)
+    if x.data_ptr() % 16:
+        x = x.contiguous(memory_format=torch.channels_last).clone(memory_format=torch.channels_last)
+    out = torch.empty(B, C // 4, H, W, 4, dtype=torch.float32, device=x.device)
+    rc = N.lib().dpft_bn_elu_pack(_ptr(x), _ptr(chan), _ptr(out), B, C, H, W, _stream(x.device))
+    N.check(rc, "dpft_bn_elu_pack")
+    return out
+
+
+def bn_elu_unaligned_(x, chan):
+    """x = ELU(x a + b) in place by torch ops, for a map the kernel cannot take (not 16-byte
+    aligned): the formula of dpft_bn_elu, shared by the eager path and the dpft::bn_elu_ op so
+    that compiled and eager forwards agree."""
+    C = x.shape[1]
+    a, b = chan[:C].view(1, C, 1, 1), chan[C:].view(1, C, 1, 1)
+    x.copy_(torch.nn.functional.elu(x * a + b))
 
 
 def channels_last(x):

@@ -1,7 +1,8 @@
 """Pose-error metrics of the evaluation scripts ("3DPE vs ref", RPE).
 
-Restated from the reference's criterions (code/models/criterions.py), same names
-and conventions, evaluation (non-training) branch:
+The reference's criterions (code/models/criterions.py) live in models/criterions.py
+(the drop-in `models.criterions` the reference's evaluate.py / convergence_basin.py
+import); this module adds the bench / evaluation bookkeeping around them:
   EPE3D_loss            criterions.py:23-46   per-sample mean |flow_gt - flow_est|_2
                                               over pixels that are not NaN / invalid
   RPE                   criterions.py:49-57   (rotation angle, |t|) of a relative pose
@@ -10,38 +11,8 @@ and conventions, evaluation (non-training) branch:
                                               frame-0 depth under T_est vs T_gt
 Host-side PyTorch (runs on whichever device the tensors are on).
 """
-import torch
-
 from .models import geometry as geo
-
-
-def EPE3D_loss(input_flow, target_flow, invalid=None):
-    epe_map = torch.norm(target_flow - input_flow, p=2, dim=1)
-    B = epe_map.shape[0]
-    bad = torch.isnan(target_flow).any(1)
-    if invalid is not None:
-        bad = bad | (invalid.view(bad.shape) > 0)
-    out = []
-    for i in range(B):
-        e = epe_map[i][~bad[i]]
-        out.append(e.mean() if e.numel() else torch.zeros((), dtype=input_flow.dtype, device=input_flow.device))
-    return torch.stack(out)
-
-
-def RPE(R, t):
-    return geo.batch_mat2angle(R), torch.norm(t.reshape(t.shape[0], 3), p=2, dim=1)
-
-
-def compute_RPE_loss(R_est, t_est, R_gt, t_gt):
-    dR, dt = geo.batch_Rt_between(R_est, t_est, R_gt, t_gt)
-    return RPE(dR, dt)
-
-
-def compute_RT_EPE_loss(R_est, t_est, R_gt, t_gt, depth0, K, invalid=None):
-    xyz = geo.batch_inverse_project(depth0, K)
-    flow_gt = geo.batch_transform_xyz(xyz, R_gt, t_gt)
-    flow_est = geo.batch_transform_xyz(xyz, R_est, t_est)
-    return EPE3D_loss(flow_est, flow_gt, invalid=invalid)
+from .models.criterions import EPE3D_loss, RPE, compute_RPE_loss, compute_RT_EPE_loss  # noqa: F401
 
 
 # ---------------------------------------------------------------- bench helpers

@@ -249,14 +249,26 @@ class LeastSquareTracking(nn.Module):
         if x.is_cuda:
             # On the GPU the encoder runs in channels_last memory format: MIOpen's NHWC
             # convolutions skip the NCHW<->NHWC transposes around every layer (13.2 ->
-            # 11.1 ms for both frames of 8 pairs at 640x480, C = 32), and the solver
-            # relayouts the NHWC features straight to its channel-quad layout
-            # (dpft_pack_features_nhwc) -- the same values, laid out differently
+            # 11.1 ms for both frames of 8 pairs at 640x480, C = 32), and the feature heads'
+            # epilogue writes the solver's channel-quad layout (_packed_features) -- the same
+            # values, laid out differently
             if not self._encoder_nhwc:
                 self.encoder.to(memory_format=torch.channels_last)
                 self._encoder_nhwc = True
             x = x.contiguous(memory_format=torch.channels_last)
-        return self.encoder(x)
+        return self.encoder(x, packed=self._packed_features(x))
+
+    def _packed_features(self, x):
+        """The U_IC solve reads the channel-quad layout; its feature heads then write it
+        directly (FeaturePyramid(packed=True): the batchnorm + ELU epilogue of each f_conv
+        head stores [B,C/4,H,W,4], dpft_bn_elu_pack) instead of NCHW features that every
+        level call would relayout (ic.LevelCall).  Needs one uncertainty plane (Cs = 1) and
+        C % 4 == 0; the features feed only the solver here (the init-pose networks read the
+        backbone maps)."""
+        e = self.encoder
+        return (x.is_cuda and self.track_type == 'U_IC' and e.feature_extract == 'conv' and e.output_C % 4 == 0
+                and e.w_uncertainty and e.uncertainty_type not in ('identity', 'feature') and e.uncertainty_C == 1
+                and not self.training and not torch.is_grad_enabled())
 
     @staticmethod
     def _inverse_depth(depth):

@@ -114,13 +114,20 @@ class FeaturePyramid(nn.Module):
         f, p = head(x).chunk(2, dim=1)
         return torch.sum(f * torch.sigmoid(p), dim=1, keepdim=True)
 
-    def forward(self, x):
+    def forward(self, x, packed=False):
+        """packed=True (the drop-in's solve path): the 'conv' feature heads write their
+        output straight in the solver's channel-quad layout [B,C/4,H,W,4] (their batchnorm +
+        ELU epilogue stores it, ConvBlock.forward_packed) where the layout applies (eval
+        mode on the device, channels_last maps, C % 4 == 0); otherwise, and for every other
+        output, the reference's [B,C,H,W]."""
         maps = []
         for s in range(4):
             x = getattr(self, f'net{s}')(x if s == 0 else self.downsample(x))
             maps.append(x)
 
-        if self.feature_extract == 'skip':
+        if packed and self.feature_extract == 'conv':
+            f = [getattr(self, f'f_conv{s}').forward_packed(m) for s, m in enumerate(maps)]
+        elif self.feature_extract == 'skip':
             f = list(maps)
         elif self.feature_extract == 'average':
             f = [m.sum(dim=1, keepdim=True) / m.shape[1] for m in maps]
@@ -552,7 +559,7 @@ class TrustRegionInverseWUncertainty(nn.Module):
         (torch_ops.py); eager, the same library call through ctypes."""
         assert sigma0 is not None and sigma1 is not None
         self._check_path(x0)
-        B, C, H, W = x0.shape
+        B, C, H, W = ic.feature_shape(x0)  # NCHW, or the channel-quad layout of a packed encoder
         kw = self._common(x0, depth0, depth1, obj_mask0, obj_mask1)
         with torch.no_grad():
             if torch.compiler.is_compiling():

@@ -2,27 +2,65 @@
 
 The per-pixel geometry of the hot path (warp, occlusion, sampling, Jacobians)
 lives in the HIP kernels; these are the small batched [B,3,3] helpers:
-  batch_euler2mat   geometry.py:447-504 ('sxyz' axes, the only ones the tracker uses)
+  batch_euler2mat   geometry.py:447-504 (every transforms3d axis convention)
+  batch_mat2euler   geometry.py:506-554
+  batch_create_transform  geometry.py:1139-1149 (kf_vo.py's 4x4 poses)
   pose_vec2mat      geometry.py:274-289 (keeps the reference's quirk: the rotation is
                     built from vec[:, 3:], the translation part -- Appendix C of SURVEY.md)
   batch_Rt_compose  geometry.py:105-123
   batch_inverse_Rt  geometry.py:87-103
   batch_Rt_between  geometry.py:125-144
 """
+import numpy as np
 import torch
 
 
-def batch_euler2mat(ai, aj, ak):
-    """Rotation matrices [B,3,3] from static x-y-z Euler angles [B] each."""
+# Euler axis conventions (transforms3d.euler, which geometry.py:447-554 follows): the 24
+# axis strings -> (first axis, parity, repetition, frame); 's' = static, 'r' = rotating frame
+_NEXT_AXIS = (1, 2, 0, 1)
+_AXES2TUPLE = {
+    'sxyz': (0, 0, 0, 0), 'sxyx': (0, 0, 1, 0), 'sxzy': (0, 1, 0, 0), 'sxzx': (0, 1, 1, 0),
+    'syzx': (1, 0, 0, 0), 'syzy': (1, 0, 1, 0), 'syxz': (1, 1, 0, 0), 'syxy': (1, 1, 1, 0),
+    'szxy': (2, 0, 0, 0), 'szxz': (2, 0, 1, 0), 'szyx': (2, 1, 0, 0), 'szyz': (2, 1, 1, 0),
+    'rzyx': (0, 0, 0, 1), 'rxyx': (0, 0, 1, 1), 'ryzx': (0, 1, 0, 1), 'rxzx': (0, 1, 1, 1),
+    'rxzy': (1, 0, 0, 1), 'ryzy': (1, 0, 1, 1), 'rzxy': (1, 1, 0, 1), 'ryxy': (1, 1, 1, 1),
+    'ryxz': (2, 0, 0, 1), 'rzxz': (2, 0, 1, 1), 'rxyz': (2, 1, 0, 1), 'rzyz': (2, 1, 1, 1)}
+
+
+def _axes(axes):
+    """(i, j, k, parity, repetition, frame) of an axis string or tuple."""
+    if isinstance(axes, str):
+        if axes.lower() not in _AXES2TUPLE:
+            raise KeyError(f"unknown Euler axes {axes!r}")
+        first, parity, rep, frame = _AXES2TUPLE[axes.lower()]
+    else:
+        if tuple(axes) not in _AXES2TUPLE.values():
+            raise KeyError(f"unknown Euler axes {axes!r}")
+        first, parity, rep, frame = axes
+    return first, _NEXT_AXIS[first + parity], _NEXT_AXIS[first - parity + 1], parity, rep, frame
+
+
+def batch_euler2mat(ai, aj, ak, axes='sxyz'):
+    """Rotation matrices [B,3,3] from Euler angles [B] each (geometry.py:447-504)."""
+    i, j, k, parity, rep, frame = _axes(axes)
+    if frame:
+        ai, ak = ak, ai
+    if parity:
+        ai, aj, ak = -ai, -aj, -ak
     si, sj, sk = torch.sin(ai), torch.sin(aj), torch.sin(ak)
     ci, cj, ck = torch.cos(ai), torch.cos(aj), torch.cos(ak)
     cc, cs, sc, ss = ci * ck, ci * sk, si * ck, si * sk
-    rows = (
-        (cj * ck, sj * sc - cs, sj * cc + ss),
-        (cj * sk, sj * ss + cc, sj * cs - sc),
-        (-sj, cj * si, cj * ci),
-    )
-    return torch.stack([torch.stack(r, 1) for r in rows], 1)
+    if rep:
+        e = ((cj, sj * si, sj * ci), (sj * sk, -cj * ss + cc, -cj * cs - sc), (-sj * ck, cj * sc + cs, cj * cc - ss))
+    else:
+        e = ((cj * ck, sj * sc - cs, sj * cc + ss), (cj * sk, sj * ss + cc, sj * cs - sc), (-sj, cj * si, cj * ci))
+    # e[a][b] is the entry at (axis a, axis b) of (i, j, k): place it at its matrix position
+    ax = (i, j, k)
+    M = [[None] * 3 for _ in range(3)]
+    for a in range(3):
+        for b in range(3):
+            M[ax[a]][ax[b]] = e[a][b]
+    return torch.stack([torch.stack(r, 1) for r in M], 1)
 
 
 def pose_vec2mat(vec, rotation_mode='euler'):
@@ -53,17 +91,30 @@ def batch_Rt_between(R0, t0, R1, t1):
     return dR, t1.reshape(-1, 3) - torch.bmm(dR, t0.reshape(-1, 3, 1)).view(-1, 3)
 
 
-def batch_mat2euler(M):
-    """Static x-y-z Euler angles (ax, ay, az) [B] each of rotations [B,3,3]
-    (geometry.py:506-554, 'sxyz': i, j, k = 0, 1, 2, no repetition / parity / frame)."""
-    cy = torch.sqrt(M[:, 0, 0] ** 2 + M[:, 1, 0] ** 2)
-    degenerate = ~(cy > 1e-8)
-    ax = torch.atan2(M[:, 2, 1], M[:, 2, 2])
-    ay = torch.atan2(-M[:, 2, 0], cy)
-    az = torch.atan2(M[:, 1, 0], M[:, 0, 0])
+def batch_mat2euler(M, axes='sxyz'):
+    """Euler angles (ax, ay, az) [B] each of rotations [B,3,3] (geometry.py:506-554); a
+    degenerate matrix (|cos| or |sin| of the middle angle below 1e-8) takes the
+    reference's gimbal-lock branch."""
+    i, j, k, parity, rep, frame = _axes(axes)
+    if rep:
+        sy = torch.sqrt(M[:, i, j] ** 2 + M[:, i, k] ** 2)
+        degenerate = ~(sy > 1e-8)
+        ax = torch.atan2(M[:, i, j], M[:, i, k])
+        ay = torch.atan2(sy, M[:, i, i])
+        az = torch.atan2(M[:, j, i], -M[:, k, i])
+    else:
+        cy = torch.sqrt(M[:, i, i] ** 2 + M[:, j, i] ** 2)
+        degenerate = ~(cy > 1e-8)
+        ax = torch.atan2(M[:, k, j], M[:, k, k])
+        ay = torch.atan2(-M[:, k, i], cy)
+        az = torch.atan2(M[:, j, i], M[:, i, i])
     if bool(degenerate.any()):
-        ax = torch.where(degenerate, torch.atan2(-M[:, 1, 2], M[:, 1, 1]), ax)
+        ax = torch.where(degenerate, torch.atan2(-M[:, j, k], M[:, j, j]), ax)
         az = torch.where(degenerate, torch.zeros_like(az), az)
+    if parity:
+        ax, ay, az = -ax, -ay, -az
+    if frame:
+        ax, az = az, ax
     return ax, ay, az
 
 
@@ -89,3 +140,15 @@ def batch_transform_xyz(xyz, R, t):
     """R xyz + t for [B,3,H,W] points (geometry.py:376-399, without the Jacobian)."""
     B, _, H, W = xyz.shape
     return (torch.bmm(R, xyz.view(B, 3, -1)) + t.reshape(B, 3, 1)).view(B, 3, H, W)
+
+
+def batch_create_transform(trs, rot):
+    """4x4 homogeneous transform(s) from a translation and a rotation (geometry.py:1139-1149):
+    numpy [3] + [3,3] -> [4,4]; torch [B,3] + [B,3,3] -> [B,4,4] on rot's device."""
+    if isinstance(trs, np.ndarray):
+        top = np.hstack((rot, trs.reshape(3, 1)))
+        return np.vstack((top, np.hstack((np.zeros([1, 3]), np.ones([1, 1])))))
+    B = trs.shape[0]
+    top = torch.cat((rot, trs.unsqueeze(2)), dim=2)
+    bot = torch.cat((torch.zeros(B, 1, 3), torch.ones(B, 1, 1)), 2).to(top)
+    return torch.cat((top, bot), dim=1)

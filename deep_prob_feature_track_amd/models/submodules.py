@@ -44,17 +44,36 @@ class ConvBlock(nn.Sequential):
     two elementwise kernels; otherwise, or for a layout the kernel does not take, the
     modules run in turn."""
 
-    def forward(self, x):
-        if len(self) == 3 and isinstance(self[1], nn.BatchNorm2d) and isinstance(self[2], nn.ELU) \
-                and self[2].alpha == 1.0 and not self.training and x.is_cuda and not torch.is_grad_enabled():
+    def _fusable(self, x):
+        return (len(self) == 3 and isinstance(self[1], nn.BatchNorm2d) and isinstance(self[2], nn.ELU)
+                and self[2].alpha == 1.0 and not self.training and x.is_cuda and not torch.is_grad_enabled())
+
+    def forward_packed(self, x):
+        """The block's output in the solver's channel-quad layout [B,C/4,H,W,4] when the
+        epilogue can write it (dpft_bn_elu_pack: the batchnorm + ELU of a channels_last
+        conv output stored out of place, no separate relayout pass); otherwise forward(x),
+        [B,C,H,W].  Same values either way."""
+        if self._fusable(x):
             y = self[0](x)
-            if torch.compiler.is_compiling():  # traced: the dpft::bn_elu_ op (torch_ops.py)
-                if torch_ops.bn_elu_applies(y, self[1]):
-                    torch.ops.dpft.bn_elu_(y, torch_ops.bn_coeffs(self[1]))
-                    return y
-            elif ic.bn_elu_(y, self[1]):
+            if ic.bn_elu_pack_applies(y, self[1]):
+                if torch.compiler.is_compiling():
+                    return torch.ops.dpft.bn_elu_pack(y, torch_ops.bn_coeffs(self[1]))
+                return ic.bn_elu_pack(y, self[1])
+            return self._epilogue(y)
+        return self.forward(x)
+
+    def _epilogue(self, y):
+        if torch.compiler.is_compiling():  # traced: the dpft::bn_elu_ op (torch_ops.py)
+            if torch_ops.bn_elu_applies(y, self[1]):
+                torch.ops.dpft.bn_elu_(y, torch_ops.bn_coeffs(self[1]))
                 return y
-            return self[2](self[1](y))
+        elif ic.bn_elu_(y, self[1]):
+            return y
+        return self[2](self[1](y))
+
+    def forward(self, x):
+        if self._fusable(x):
+            return self._epilogue(self[0](x))
         return super().forward(x)
 
 

@@ -19,6 +19,32 @@ def shard_range(n_pairs, world, rank):
     return begin, begin + base + (1 if rank < extra else 0)
 
 
+def stream_calls(steps, group):
+    """Step counts of the calls that cover exactly `steps` global batches of a stream when a
+    rank solves `group` consecutive global batches per call: full calls, then one short
+    remainder call."""
+    return [group] * (steps // group) + ([steps % group] if steps % group else [])
+
+
+def stream_group(shard_pairs, batch, min_launch_pairs=64, max_batches=32):
+    """Global batches per grouped call on a rank: enough consecutive global batches of the
+    stream that one call holds >= min_launch_pairs pairs (each global batch's shard stays
+    its own independent batches of `batch` pairs, DPFT_GROUP), at most max_batches
+    independent batches per call.  With 64-pair global batches the N = 8 rank shard (8 pairs)
+    is grouped 8 at a time -- the same 64-pair launch shape as N = 1."""
+    per_step = max(1, shard_pairs // batch)
+    q = max(1, -(-min_launch_pairs // shard_pairs))
+    return max(1, min(q, max_batches // per_step))
+
+
+def stream_pair_index(step, rank_pair, global_batch, world, rank):
+    """Stream-wide index of pair `rank_pair` of `rank`'s shard in global batch `step`: the
+    order rank 0 finds the all-gathered poses of a grouped call in is rank-major, then step,
+    then shard position -- this maps a gathered row back to its pair."""
+    begin, _ = shard_range(global_batch, world, rank)
+    return step * global_batch + begin + rank_pair
+
+
 def pack_poses(R, t):
     """[B,3,3], [B,3(,1)] -> [B,12] fp32."""
     B = R.shape[0]

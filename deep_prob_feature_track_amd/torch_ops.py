@@ -11,6 +11,7 @@ the drop-in forward as one graph instead of breaking at every ctypes call:
                             -> [invD_0 .. invD_{L-1}] (+ [depth_0 .. depth_{L-1}])
   dpft::pack_features       NCHW / channels_last -> channel-quad layout [B,C/4,H,W,4]
   dpft::bn_elu_             the encoder blocks' eval-mode batchnorm + ELU, in place
+  dpft::bn_elu_pack         the feature heads' batchnorm + ELU written to the channel-quad layout
 
 The ops never synchronise: a non-finite Jacobian / residual is reported in the returned
 status word, which the caller checks once (the reference's `assert check_nan(...) == 0`,
@@ -57,7 +58,8 @@ def ic_solve_level(R: Tensor, t: Tensor, x0: Tensor, x1: Tensor, invD0: Tensor, 
 def _(R, t, x0, x1, invD0, invD1, K, sigma0, sigma1, depth0, depth1, obj_mask0, obj_mask1, iters,
       remove_tru_sigma, combine_icp, icp_weight, no_uncertainty, return_jtj):
     B = R.shape[0]
-    return (R.new_empty(B, 3, 3), R.new_empty(B, 3, 1), R.new_empty(B if return_jtj else 0, 6, 6),
+    f32 = dict(dtype=torch.float32, device=R.device)  # the real op always returns fp32 (pose_buffers)
+    return (torch.empty(B, 3, 3, **f32), torch.empty(B, 3, 1, **f32), torch.empty(B if return_jtj else 0, 6, 6, **f32),
             torch.empty(1, dtype=torch.int32, device=R.device))
 
 
@@ -116,8 +118,7 @@ def bn_elu_(x: Tensor, chan: Tensor) -> None:
     B, C, H, W = x.shape
     nhwc = ic.channels_last(x)
     if x.data_ptr() % 16:  # (the kernel's 16-byte accesses; conv outputs are allocator-aligned)
-        a, b = chan[:C].view(1, C, 1, 1), chan[C:].view(1, C, 1, 1)
-        x.copy_(torch.nn.functional.elu(x * a + b))
+        ic.bn_elu_unaligned_(x, chan)  # the same torch formula the eager path takes here
         return
     rc = ic.N.lib().dpft_bn_elu(ic._ptr(x), ic._ptr(chan), x.numel(), C, 1 if nhwc else H * W, 1 if nhwc else 0,
                                 ic._stream(x.device))
@@ -127,6 +128,25 @@ def bn_elu_(x: Tensor, chan: Tensor) -> None:
 @bn_elu_.register_fake
 def _(x, chan):
     return None
+
+
+@torch.library.custom_op("dpft::bn_elu_pack", mutates_args=())
+def bn_elu_pack(x: Tensor, chan: Tensor) -> Tensor:
+    """ELU(x a + b) of a channels_last map, out of place in the channel-quad layout
+    [B,C/4,H,W,4] (dpft_bn_elu_pack; ic.bn_elu_pack_applies decides)."""
+    B, C, H, W = x.shape
+    if x.data_ptr() % 16:
+        x = x.clone(memory_format=torch.channels_last)
+    out = torch.empty(B, C // 4, H, W, 4, dtype=torch.float32, device=x.device)
+    rc = ic.N.lib().dpft_bn_elu_pack(ic._ptr(x), ic._ptr(chan), ic._ptr(out), B, C, H, W, ic._stream(x.device))
+    ic.N.check(rc, "dpft_bn_elu_pack")
+    return out
+
+
+@bn_elu_pack.register_fake
+def _(x, chan):
+    B, C, H, W = x.shape
+    return x.new_empty(B, C // 4, H, W, 4)
 
 
 def bn_elu_applies(x, bn):

@@ -280,6 +280,17 @@ int dpft_pack_features_nhwc(const float* src, float* dst, int32_t B, int32_t C, 
 int dpft_bn_elu(float* x, const float* chan, int64_t n, int32_t C, int64_t inner, int32_t nhwc, void* hip_stream);
 
 /*
+ * The feature heads' epilogue writing the solver's layout: the eval-mode BatchNorm + ELU
+ * of dpft_bn_elu applied to a channels_last conv output x [B,H,W,C] (the f_conv heads,
+ * reference algorithms.py:1273-1277 with convLayer submodules.py:25-39), written OUT OF
+ * PLACE to the channel-quad layout out [B,C/4,H,W,4] (DPFT_FEATURES_C4) -- the same values
+ * dpft_bn_elu followed by dpft_pack_features_nhwc give, in one read and one write instead of
+ * two of each.  C % 4 == 0; x, out 16-byte aligned, not aliased.
+ */
+int dpft_bn_elu_pack(const float* x, const float* chan, float* out, int32_t B, int32_t C, int32_t H, int32_t W,
+                     void* hip_stream);
+
+/*
  * Jacobian API, materialised -- the reference solver's methods that the fused solve
  * never needs (it keeps J in registers); kept for callers and tests that inspect J.
  *  dpft_feature_gradient    feature_gradient (algorithms.py:1844-1865): unit-normalised

@@ -1,8 +1,9 @@
 """Deterministic solver-level inputs for the parity fixtures.
 
 Test infrastructure only. Every tensor is built from the five TUM fr1/desk
-example frames the reference ships (`code/data/data_examples/TUM`, stored here
-as `tum_fr1_desk_frames.npz`) with exactly-rounded IEEE ops only (+, -, *, /,
+example frames the reference ships (`code/data/data_examples/TUM`, stored in the
+package as `deep_prob_feature_track_amd/data/tum_fr1_desk_frames.npz`, loaded by
+`deep_prob_feature_track_amd.examples`) with exactly-rounded IEEE ops only (+, -, *, /,
 floor, abs, min/max, clip), so the same bits come out on any host with the
 same numpy.  SHA-256 digests of every tensor are stored beside the golden
 outputs and re-checked before a comparison.
@@ -22,22 +23,17 @@ batch-global min and max are zeroed; pyramids are max-pools of level 0
 """
 import hashlib
 import os
+import sys
 
 import numpy as np
 
-HERE = os.path.dirname(os.path.abspath(__file__))
-FRAMES = os.path.join(HERE, "tum_fr1_desk_frames.npz")
-K_FULL = np.array([525.0, 525.0, 319.5, 239.5], dtype=np.float32)  # code/test.py:68
+ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+if ROOT not in sys.path:
+    sys.path.insert(0, ROOT)
+from deep_prob_feature_track_amd.examples import (K_FULL, ORDERED_PAIRS, color_float, depth_m,  # noqa: E402,F401
+                                                  frames, synthetic_weights)
+
 SIGMA_LO, SIGMA_HI = np.float32(0.5), np.float32(1.5)
-
-_frames_cache = {}
-
-
-def frames():
-    if "f" not in _frames_cache:
-        z = np.load(FRAMES, allow_pickle=False)
-        _frames_cache["f"] = (z["color"], z["depth"])
-    return _frames_cache["f"]
 
 
 def _pool_sum(a, k):
@@ -61,50 +57,6 @@ def grey_int(idx, base_down=1):
     c = color[idx].astype(np.int64)
     g = 77 * c[..., 0] + 150 * c[..., 1] + 29 * c[..., 2]
     return _pool_sum(g, base_down), base_down * base_down
-
-
-def depth_m(idx, base_down=1):
-    _, depth = frames()
-    d = depth[idx][::base_down, ::base_down].astype(np.float32) / np.float32(5e3)
-    return np.clip(d, np.float32(0.5), np.float32(5.0)).astype(np.float32)
-
-
-def color_float(idx, base_down=1):
-    """[3, H, W] RGB in [0, 1] (nearest subsampling; uint8 / 255 in fp32)."""
-    color, _ = frames()
-    c = color[idx][::base_down, ::base_down].astype(np.float32)
-    return (np.moveaxis(c, -1, 0) / np.float32(255.0)).astype(np.float32)
-
-
-def synthetic_weights(key, shape, gain=1.5):
-    """Deterministic stand-in for trained weights (the checkpoints are absent).
-
-    Conv / linear weights: hashed-integer uniform values with variance
-    gain^2 / fan_in; biases 0; BatchNorm at identity statistics.  Integer mixing
-    and exactly-rounded float32 ops only, so every host produces the same bits."""
-    shape = tuple(int(v) for v in shape)
-    leaf = key.rsplit(".", 1)[-1]
-    if leaf == "num_batches_tracked":
-        return np.zeros(shape, np.int64)
-    if leaf in ("running_mean", "bias"):
-        return np.zeros(shape, np.float32)
-    if leaf == "running_var":
-        return np.ones(shape, np.float32)
-    if len(shape) == 1:  # BatchNorm weight
-        return np.ones(shape, np.float32)
-    if "sigma_conv" in key:  # keep the uncertainty heads off their clamps
-        gain = 0.1
-    n = int(np.prod(shape))
-    fan_in = n // shape[0]
-    seed = np.uint64(sum((k + 1) * ord(ch) for k, ch in enumerate(key)))
-    h = np.arange(n, dtype=np.uint64) * np.uint64(2654435761) + seed * np.uint64(40503)
-    h &= np.uint64(0xFFFFFFFF)
-    for sh in (16, 13, 16):  # integer avalanche mix (exact, host-independent)
-        h ^= h >> np.uint64(sh)
-        h = (h * np.uint64(0x45D9F3B)) & np.uint64(0xFFFFFFFF)
-    u = (h >> np.uint64(8)).astype(np.float32) / np.float32(16777216.0) - np.float32(0.5)  # [-0.5, 0.5)
-    scale = np.float32(gain * np.sqrt(12.0 / fan_in))
-    return (u * scale).astype(np.float32).reshape(shape)
 
 
 _feat_cache = {}
@@ -278,7 +230,6 @@ def perturbations(n, rot, trs, k0=0):
     return out
 
 
-ORDERED_PAIRS = [(i, j) for i in range(5) for j in range(5) if i != j]  # cfg3's 20 ordered pairs
 CFG4_PAIRS = [(0, 1), (1, 3), (2, 4), (4, 0)]
 
 # Named cases shared by the fixture generator and the tests.
@@ -314,3 +265,7 @@ CASES = {
 }
 # cfg4's full batch: 256 masked pairs (80 distinct: the 20 ordered pairs x 4 flip codes), identity start
 CASES["cfg4_sweep256_160x120_c8"] = sweep_spec(256)
+# cfg4's batch from two perturbed start sets (convergence_basin.py:337-418's 1-D axes applied
+# to the identity start): a 0.1 rad rotation about x, a 0.1 m translation along z
+CASES["cfg4_sweep256_rotx10_160x120_c8"] = dict(sweep_spec(256), init=[([0.1, 0.0, 0.0], [0.0, 0.0, 0.0])] * 256)
+CASES["cfg4_sweep256_tz10_160x120_c8"] = dict(sweep_spec(256), init=[([0.0, 0.0, 0.0], [0.0, 0.0, 0.1])] * 256)

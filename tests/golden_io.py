@@ -44,3 +44,32 @@ def init_pose(case, dtype=torch.float32, device="cpu"):
     R = torch.from_numpy(case["R_init"]).to(device=device, dtype=dtype)
     t = torch.from_numpy(case["t_init"]).to(device=device, dtype=dtype)
     return R, t
+
+
+def noise_floor(z, prec="f32"):
+    """The reference's own `prec` noise floor per iteration, [iters, B] (None if the
+    fixture has none): how far its trajectory moves when only rounding changes -- max over
+    the jittered-start runs (start translation moved by U(+-3.4e-8), the measured one-step
+    deviation of the HIP solve from the reference) and the one-thread run of max(|dR|, |dt|)
+    against the fixture's fp32 run (tests/golden/gen_golden.py --noise); prec="f64": the
+    fp64 jittered-start runs (start moved by U(+-1e-15), --noise64)."""
+    if f"{prec}_jitter_R" not in z:
+        return None
+    R, t = z[f"{prec}_R"], z[f"{prec}_t"]
+    dR = np.abs(z[f"{prec}_jitter_R"] - R[None]).max(axis=(0, 3, 4))
+    dt = np.abs(z[f"{prec}_jitter_t"] - t[None]).max(axis=(0, 3))
+    fl = np.maximum(dR, dt)
+    if prec == "f32" and "f32_t1_R" in z:
+        fl = np.maximum(fl, np.maximum(np.abs(z["f32_t1_R"] - R).max(axis=(2, 3)), np.abs(z["f32_t1_t"] - t).max(axis=2)))
+    # per iteration, the largest move of any pair: which pair a rounding change hits is itself
+    # chance (the batch-global sigma_r extrema sit in one pair's pixels; B = 256 shows it: the
+    # trials move a few pairs each, different ones), so the floor is the batch's, not a pair's
+    return np.broadcast_to(fl.max(axis=1, keepdims=True), fl.shape).copy()
+
+
+def pose_deviation(R, t, z, prec="f32", i=-1):
+    """Per pair max(|dR|, |dt|) of poses (R [B,3,3], t [B,3(,1)], numpy or torch) against the
+    fixture's `prec` run at iteration i."""
+    R = np.asarray(R.cpu() if hasattr(R, "cpu") else R).reshape(-1, 3, 3)
+    t = np.asarray(t.cpu() if hasattr(t, "cpu") else t).reshape(-1, 3)
+    return np.maximum(np.abs(R - z[f"{prec}_R"][i]).max(axis=(1, 2)), np.abs(t - z[f"{prec}_t"][i]).max(axis=1))

@@ -24,6 +24,13 @@ def test_library_exports_every_declared_symbol():
     assert L.dpft_version() == N.ABI_VERSION
 
 
+def test_control_area_size_matches_the_library():
+    """The Python side zeroes only the workspace's control prefix of private workspaces
+    (ic.LevelCall): that prefix must be the library's kCtrlBytes, or stale completion
+    counters would make the last-workgroup handshake misfire."""
+    assert N.CTRL_BYTES == N.lib().dpft_preprocess_workspace_size()
+
+
 def test_invalid_descriptor_is_rejected_without_device_work():
     import ctypes
     L = N.lib()

@@ -87,3 +87,58 @@ def test_channels_last_encoder_matches_nchw():
         f_b, s_b, _ = enc(x.contiguous(memory_format=torch.channels_last))
     for a, b in zip(f_a + s_a, f_b + s_b):
         torch.testing.assert_close(b, a, rtol=1e-4, atol=1e-5 * a.abs().max().item())
+
+
+@pytest.mark.parametrize("cout,H,W", [(32, 48, 64), (8, 15, 20), (16, 7, 9)])
+def test_bn_elu_pack_equals_bn_elu_then_pack(cout, H, W):
+    """The feature heads' epilogue written to the channel-quad layout (dpft_bn_elu_pack) is
+    bit for bit the in-place epilogue followed by the relayout (dpft_bn_elu +
+    dpft_pack_features_nhwc), and ConvBlock.forward_packed returns it."""
+    from deep_prob_feature_track_amd import ic
+    dev = _dev()
+    blk = _block(24, cout, 1, 1, dev, seed=cout + H).to(memory_format=torch.channels_last)
+    x = torch.randn(3, 24, H, W, device=dev).contiguous(memory_format=torch.channels_last)
+    with torch.no_grad():
+        conv = blk[0](x)
+        y = conv.clone()
+        assert ic.bn_elu_(y, blk[1])
+        ref = ic.pack_features(y)
+        got = ic.bn_elu_pack(conv, blk[1])
+        via_block = blk.forward_packed(x)
+    assert got.shape == (3, cout // 4, H, W, 4)
+    assert torch.equal(got, ref) and torch.equal(via_block, ref)
+    assert torch.equal(ic.unpack_features(got), y.contiguous())
+
+
+def test_dropin_forward_with_packed_encoder_equals_nchw_features():
+    """LeastSquareTracking's feature heads write the solver's layout (no relayout pass in
+    the forward): the poses equal those of the same model fed NCHW features bit for bit
+    (the same feature values, the same kernels)."""
+    from deep_prob_feature_track_amd.examples import K_FULL, color_float, depth_m, load_synthetic_weights
+    from deep_prob_feature_track_amd.models.LeastSquareTracking import LeastSquareTracking, default_options
+    dev = _dev()
+    net = LeastSquareTracking("ConvRGBD2", "laplacian", 3, "None", "Direct-Nodamping",
+                              options=default_options(feature_channel=16, uncertainty_channel=1,
+                                                      feature_extract="conv", remove_tru_sigma=True))
+    net = load_synthetic_weights(net).to(dev).eval()
+    pairs = [(0, 1), (2, 4)]
+    img0 = torch.stack([torch.from_numpy(color_float(i, 2)) for i, _ in pairs]).to(dev)
+    img1 = torch.stack([torch.from_numpy(color_float(j, 2)) for _, j in pairs]).to(dev)
+    d0 = torch.stack([torch.from_numpy(depth_m(i, 2))[None] for i, _ in pairs]).to(dev)
+    d1 = torch.stack([torch.from_numpy(depth_m(j, 2))[None] for _, j in pairs]).to(dev)
+    K = torch.from_numpy(K_FULL / 2).repeat(len(pairs), 1).to(dev)
+    with torch.no_grad():
+        for _ in range(2):  # MIOpen settles on its convolution algorithms over the first calls
+            net(img0, img1, d0, d1, K)
+        R, t = net(img0, img1, d0, d1, K)
+        prep = net.prepare(img0, img1, d0, d1)
+        assert prep[2][0].dim() == 5, "the drop-in's features should come packed"
+        net._packed_features = lambda x: False
+        R2, t2 = net(img0, img1, d0, d1, K)
+        prep2 = net.prepare(img0, img1, d0, d1)
+        assert prep2[2][0].dim() == 4
+    from deep_prob_feature_track_amd import ic
+    for l in range(4):  # the same feature values in the two layouts
+        assert torch.equal(ic.unpack_features(prep[2][l]), prep2[2][l].contiguous()), f"level {l} x0"
+        assert torch.equal(ic.unpack_features(prep[3][l]), prep2[3][l].contiguous()), f"level {l} x1"
+    assert torch.equal(R, R2) and torch.equal(t, t2)

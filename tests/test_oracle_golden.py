@@ -16,7 +16,8 @@ import recipe
 from oracle import ic_oracle as O
 
 CASES = list(recipe.CASES)
-SLOW_F64 = {"cfg3_b8_640x480_c32"}  # ~35 s per fp64 oracle run on 8 CPU threads
+SLOW_F64 = {"cfg3_b8_640x480_c32",  # ~35 s per fp64 oracle run on 8 CPU threads
+            "cfg4_sweep256_160x120_c8", "cfg4_sweep256_rotx10_160x120_c8", "cfg4_sweep256_tz10_160x120_c8"}
 
 
 def run_oracle(name, dtype):
@@ -47,7 +48,7 @@ def test_oracle_matches_reference(name, prec):
     """
     dtype = torch.float64 if prec == "f64" else torch.float32
     if name in SLOW_F64 and prec == "f64":
-        pytest.skip("8 pairs at 640x480 in fp64: the fp64 oracle is pinned by the other cases")
+        pytest.skip("a large batch in fp64: the fp64 oracle is pinned by the other cases")
     if f"{prec}_R" not in golden_io.load(name, check_digests=False)[1]:
         pytest.skip(f"reference cannot run {prec} for {name}")
     case, z, trace = run_oracle(name, dtype)
@@ -58,19 +59,21 @@ def test_oracle_matches_reference(name, prec):
     # its fp64 one; measured worst here 8.9e-5 (cfg4_pert20)
     loose = (2e-5 if prec == "f64" else 1e-4) if fragile else tight
     L = case["levels"]
-    # where the reference itself is more sensitive than `loose` (its final pose moves by
-    # more under a 1e-7 start change: tests/golden/gen_golden.py --jitter), a chained
-    # trajectory is bounded per pair by twice that envelope; the restarted test is exact
-    env = 0.0
-    if prec == "f32" and "f32_jitter_R" in z:
-        env = np.maximum(np.abs(z["f32_jitter_R"] - z["f32_R"][-1][None]).max(axis=(0, 2, 3)),
-                         np.abs(z["f32_jitter_t"] - z["f32_t"][-1][None]).max(axis=(0, 2)))
+    # where the reference itself is more sensitive than `loose` at an iteration (its own
+    # trajectory moves by more when only rounding changes: golden_io.noise_floor, per
+    # iteration and pair), a chained trajectory is bounded there by twice that floor; the
+    # restarted test below is exact
+    floor = golden_io.noise_floor(z, prec)
     prev_dev = 0.0
     for i, tr in enumerate(trace):
         dR = np.abs(tr["R"].numpy() - z[f"{prec}_R"][i]).max(axis=(1, 2))
         dt = np.abs(tr["t"].numpy() - z[f"{prec}_t"][i]).max(axis=1)
-        tol = tight if i == 0 else np.maximum(loose, 2.0 * env)
+        tol = tight if i == 0 else np.maximum(loose, 2.0 * floor[i]) if floor is not None else loose
         assert (dR <= tol).all() and (dt <= tol).all(), f"{name} {prec} iter {i}: |dR|={dR.max():.3e} |dt|={dt.max():.3e}"
+        over = np.flatnonzero(np.maximum(dR, dt) > 1e-4)
+        if over.size:
+            print(f"{name} {prec} iter {i}: pairs beyond 1e-4 (within 2x the reference's noise floor):",
+                  {int(b): f"{max(dR[b], dt[b]):.2e} (floor {floor[i][b]:.2e})" for b in over})
         jtj_ref = z[f"{prec}_jtj"][i]
         rel = np.abs(tr["JtJ"].numpy() - jtj_ref).max() / np.abs(jtj_ref).max()
         if i == 0 or prev_dev <= 1e-5:  # normal equations compared where the poses still agree

@@ -143,3 +143,55 @@ def test_two_rank_gather_results_ragged_shards(n_pairs):
     owner = torch.cat([torch.full((e - b,), r, dtype=torch.int32) for r, (b, e) in enumerate(spans)])
     assert torch.equal(res["status"], owner)
 
+
+
+def _worker_stream(rank, world, port, q, global_batch, batch, min_launch, steps):
+    """bench.py's grouped stream on `world` gloo ranks: each rank solves its shard of Q
+    consecutive global batches per call (shard.stream_group / stream_calls), the poses of a
+    call are all-gathered asynchronously; a pose here encodes its stream pair (R = index,
+    t = step) so rank 0 can check the coverage and the row order."""
+    torch.set_num_threads(1)
+    dist.init_process_group("gloo", init_method=f"file://{port}", rank=rank, world_size=world)
+    try:
+        b, e = shard.shard_range(global_batch, world, rank)
+        n_r = e - b
+        Q = shard.stream_group(n_r, batch, min_launch)
+        rows, step0 = [], 0
+        for qn in shard.stream_calls(steps, Q):
+            idx = torch.tensor([float(shard.stream_pair_index(step0 + k, i, global_batch, world, rank))
+                                for k in range(qn) for i in range(n_r)])
+            R = idx.view(-1, 1, 1) * torch.ones(1, 3, 3)
+            t = torch.tensor([float(step0 + k) for k in range(qn) for _ in range(n_r)]).view(-1, 1) * torch.ones(1, 3)
+            out, work = shard.gather_poses(R, t, async_op=True)
+            R.zero_()  # the next call overwrites the poses while the gather runs
+            work.wait()
+            rows.append(out.numpy().copy())
+            step0 += qn
+        if rank == 0:
+            q.put((Q, rows))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_two_rank_grouped_stream_covers_every_pair_once():
+    """The N > 1 bench step shape: 2 ranks, global batches of 4 pairs (2 per rank), grouped 3
+    global batches per call (>= 6 pairs per call), 7 global batches (calls of 3, 3 and a
+    remainder of 1): the gathered rows cover every stream pair exactly once, in the
+    rank-major / step / shard order that shard.stream_pair_index names."""
+    import numpy as np
+    world, gb, batch, min_launch, steps = 2, 4, 2, 6, 7
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker_stream, args=(r, world, port, q, gb, batch, min_launch, steps))
+             for r in range(world)]
+    for p in procs:
+        p.start()
+    Q, rows = q.get(timeout=120)
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    assert Q == 3 and [r.shape[0] for r in rows] == [12, 12, 4]
+    seen = np.concatenate([r[:, 0] for r in rows])
+    assert sorted(seen.astype(int).tolist()) == list(range(steps * gb))
+    assert np.all(np.floor(seen / gb) == np.concatenate([r[:, 9] for r in rows]))  # pair i of step s: s*gb + ...

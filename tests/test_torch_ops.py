@@ -120,3 +120,30 @@ def test_dropin_traces_without_graph_breaks_and_matches_eager(name):
                 from deep_prob_feature_track_amd import ic
                 ic.check_status(m.last_status)
     np.testing.assert_equal(Re.cpu().numpy().shape[1:], (3, 3))
+
+
+@pytest.mark.gpu
+def test_compiled_forward_reports_nonfinite_in_last_status():
+    """Under torch.compile the drop-in cannot raise inside the graph (no host read there):
+    a non-finite Jacobian / residual is reported in `model.last_status`, a device tensor the
+    caller checks with ic.check_status -- as eager forward's
+    AssertionError (the reference's `assert check_nan(...) == 0`, algorithms.py:886, 1988)."""
+    from deep_prob_feature_track_amd import _native as Nn
+    from deep_prob_feature_track_amd import ic
+    dev = _dev()
+    m, T = _model("convrgbd2_c8", dev)
+    img0 = T["img0"].clone()
+    img0[:, :, 5:9, 7:11] = float("nan")
+    args = (img0, T["img1"], T["depth0"], T["depth1"], T["K"])
+    with torch.no_grad():
+        with pytest.raises(AssertionError):
+            m(*args)
+        torch._dynamo.reset()
+        mc = torch.compile(m, backend="aot_eager")
+        mc(*args)
+    torch.cuda.synchronize()
+    st = m.last_status
+    assert isinstance(st, torch.Tensor) and st.is_cuda, type(st)
+    assert int(st.cpu()[0]) & Nn.STATUS_NONFINITE
+    with pytest.raises(AssertionError):
+        ic.check_status(st)

@@ -43,7 +43,10 @@ __device__ inline v4i rsrc(const void* p, uint32_t bytes) {
 // row bands x 11 strips = 33 segments with common row cuts (neighbouring strips march the
 // same rows at the same time), wave w < 32 owns segment w, the 33rd is split 5 rows a wave
 // and marched after it; 5: as 0 without the XCD-aware workgroup remap; 6: as 4 with a
-// workgroup barrier every row (the 4 waves -- mostly 4 adjacent strips -- in lockstep)
+// workgroup barrier every row (the 4 waves -- mostly 4 adjacent strips -- in lockstep);
+// 7: as 4 plus the real kernel's two trailing tap loads per group, every lane re-requesting
+// its leading pair (the tap cache's branch-free hit path: L1 hits); 8: as 4 plus the two
+// trailing loads from one lane in eight only (EXEC-masked: the data path skips the hit lanes)
 template <int G, int MODE = 0>
 __global__ __launch_bounds__(256) void march(const float* f0, const float* f1, float* out, float rot, float shift) {
   __shared__ float pin[80 * 1024 / 4];  // the real kernel's LDS footprint: 2 workgroups per CU
@@ -59,7 +62,7 @@ __global__ __launch_bounds__(256) void march(const float* f0, const float* f1, f
   const uint32_t frame = (uint32_t)H * W * C * 4;
   const v4i r0 = rsrc(f0 + (size_t)b * H * W * C, frame), r1 = rsrc(f1 + (size_t)b * H * W * C, frame);
   f32x4 acc = {0.f, 0.f, 0.f, 0.f};
-  constexpr bool GP = MODE == 4 || MODE == 6;
+  constexpr bool GP = MODE == 4 || MODE == 6 || MODE == 7 || MODE == 8;
   const int nunits = GP ? 160 + 5 : uend - ubeg;
   for (int i = 0; i < nunits; ++i) {
     int s, y;
@@ -78,7 +81,7 @@ __global__ __launch_bounds__(256) void march(const float* f0, const float* f1, f
     const int tx = MODE == 2 ? min(xc, W - 2) : min(max((int)floorf(fu), 0), W - 2), ty = min(max((int)floorf(fv) + 1, 0), H - 1);
     // all 24 loads of the row in flight in every layout (equal memory-level parallelism);
     // a group's chunks are issued back to back (same cache lines)
-    f32x4 l[3 * C / 4];
+    f32x4 l[5 * C / 4];
 #pragma unroll
     for (int g = 0; g < NG; ++g) {
       const int gp = g * H * W;
@@ -91,11 +94,22 @@ __global__ __launch_bounds__(256) void march(const float* f0, const float* f1, f
         } else {
           l[3 * (g * PER + k) + 1] = l[3 * (g * PER + k) + 2] = f32x4{0.f, 0.f, 0.f, 0.f};
         }
+        f32x4& t0 = l[3 * C / 4 + 2 * (g * PER + k)];
+        f32x4& t1 = l[3 * C / 4 + 2 * (g * PER + k) + 1];
+        t0 = t1 = f32x4{0.f, 0.f, 0.f, 0.f};
+        if (MODE == 7) {
+          t0 = bload(r1, ((gp + ty * W + tx) * G) * 4 + 16 * k, 0, 0);
+          t1 = bload(r1, ((gp + ty * W + tx + 1) * G) * 4 + 16 * k, 0, 0);
+        } else if (MODE == 8 && (lane & 7) == 0) {
+          const int tyt = max(ty - 1, 0);
+          t0 = bload(r1, ((gp + tyt * W + tx) * G) * 4 + 16 * k, 0, 0);
+          t1 = bload(r1, ((gp + tyt * W + tx + 1) * G) * 4 + 16 * k, 0, 0);
+        }
       }
     }
     asm volatile("" ::: "memory");
 #pragma unroll
-    for (int k = 0; k < 3 * C / 4; ++k) acc += l[k];
+    for (int k = 0; k < 5 * C / 4; ++k) acc += l[k];
   }
   pin[threadIdx.x] = acc.x;
   if (acc.x + acc.y + acc.z + acc.w == 12345.f) out[0] = pin[(threadIdx.x + 1) & 255];
@@ -118,7 +132,7 @@ void run(const float* f0, const float* f1, float* out) {
   const double us = ms * 1e3 / reps;
   const double alg = 2.0 * NP * H * W * C * 4;  // f0 + f1 once each
   static const char* modes[] = {"marching", "f0 only", "f1 at own column", "64-col strips", "grid 3x11 + pool",
-                                "no XCD remap", "grid + row barrier"};
+                                "no XCD remap", "grid + row barrier", "grid + re-requests", "grid + 1/8 trailing"};
   printf("G=%2d %-17s: %7.1f us per launch, %6.0f GB/s algorithmic (f0 + f1)\n", G, modes[MODE], us,
          (MODE == 1 ? alg / 2 : alg) / (us * 1e-6) / 1e9);
 }
@@ -140,7 +154,17 @@ int main(int argc, char** argv) {
       case 3: run<4, 3>(f0, f1, out); break;
       case 4: run<4, 4>(f0, f1, out); break;
       case 5: run<4, 5>(f0, f1, out); break;
+      case 7: run<4, 7>(f0, f1, out); break;
+      case 8: run<4, 8>(f0, f1, out); break;
       default: run<4, 6>(f0, f1, out); break;
+    }
+    return 0;
+  }
+  if (only == -2) {  // the tap-cache trailing-load question only
+    for (int rep = 0; rep < 3; ++rep) {
+      run<4, 4>(f0, f1, out);
+      run<4, 7>(f0, f1, out);
+      run<4, 8>(f0, f1, out);
     }
     return 0;
   }
