@@ -629,13 +629,15 @@ __device__ __forceinline__ IcpTerm icp_pixel(float xr, float yr, float d0, const
   // ||diff|| > 0.1 occlusion: the tap vertices) and stay op for op.  These only scale
   // continuous values: the constants are folded (depth / 525 * 5.5 -> depth * (5.5 / 525),
   // depth^2 * 0.4 / (525 * 1.2) -> depth^2 * (0.4 / 630)) and the seven divisions by
-  // sigma_icp + 1e-8 (965-966) are one reciprocal and seven products (each within an ulp
-  // of the quotient; the JtJ / JtR bounds are 1e-5 / 1e-4 relative)
+  // sigma_icp + 1e-8 (965-966) are one reciprocal and seven products (within a few ulp of
+  // the quotients; the JtJ / JtR bounds are 1e-5 / 1e-4 relative)
   constexpr float kSxy = 5.5f / 525.0f, kSz = 0.4f / (525.0f * 1.2f);
   const float sxy = d0 * kSxy;
   const float sz = (d0 * d0) * kSz;
   const float cov = (((n0 * sxy) * sxy) * n0 + ((n1 * sxy) * sxy) * n1) + ((n2 * sz) * sz) * n2;
-  const float rsig = wgt / (sqrtf(cov + 1e-8f) + 1e-8f);  // w / sigma: the ScaleNet weight folded in
+  // w / sigma (the ScaleNet weight folded in) by the hardware square root and reciprocal
+  // (1 ulp each, no IEEE division / sqrt sequences): continuous weights only
+  const float rsig = wgt * __builtin_amdgcn_rcpf(__builtin_amdgcn_sqrtf(cov + 1e-8f) + 1e-8f);
   IcpTerm o;
   o.J[0] = (n2 * V0y - n1 * V0z) * rsig;
   o.J[1] = (n0 * V0z - n2 * V0x) * rsig;

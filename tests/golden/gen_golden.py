@@ -21,14 +21,16 @@ pose's (double) grid (algorithms.py:2006), which grid_sample refuses, so the har
 casts the sampled map to the grid's dtype inside `geometry.warp_features` (a 0/1 mask is
 exact in both precisions; every other call already has matching dtypes).
 
-`--noise` adds the reference's own fp32 noise floor to a fixture, per iteration and pair
-(tests bound chained trajectories by it where it exceeds 1e-4): NOISE_TRIALS runs whose
-first Gauss-Newton update is moved by U(+-JITTER_ABS) per translation coordinate --
+`--noise` adds the reference's own fp32 noise floor to a fixture, per iteration (tests bound
+chained trajectories by it where it exceeds 1e-4): NOISE_TRIALS runs in which EVERY
+Gauss-Newton update's pose (R and t entries) is moved by fresh U(+-JITTER_ABS) noise --
 JITTER_ABS is the measured one-step deviation of the HIP solve from the reference (3.4e-8,
-tests/test_oracle_golden.py), applied where that deviation arises (after a step; a moved
-START would leave the identity pose, where the warp is exact and the clipped sigma plateaus
-sit at the batch extrema, a discontinuity the solve itself never crosses) -- and one run
-on a single thread (SURVEY App. B's 1-vs-N-thread spread).  `--noise64` adds the fp64
+tests/test_oracle_golden.py), applied where and as often as that deviation arises (after
+each step: an fp32 solve that sums in another order differs from the reference by that much
+at every iteration; a moved START would instead leave the identity pose, where the warp is
+exact and the clipped sigma plateaus sit at the batch extrema, a discontinuity the solve
+itself never crosses) -- and one run on a single thread (SURVEY App. B's 1-vs-N-thread
+spread).  `--noise64` adds the fp64
 floor the same way (1e-16: the truncated-sigma equality tests make the fp64 trajectory
 chaotic too).
 
@@ -87,6 +89,8 @@ def import_reference():
 
 
 def run_case(torch, A, name, dtype, perturb_first=None):
+    """perturb_first: (numpy Generator, amplitude) -- every update's pose moved by fresh
+    uniform noise of that amplitude (the --noise / --noise64 runs); None: the plain run."""
     spec = recipe.CASES[name]
     opt = OPTIONS[name]
     case = recipe.make_case(**spec)
@@ -129,8 +133,11 @@ def _run_case(torch, A, name, dtype, spec, opt, case, perturb_first=None):
 
             def gn(JtJ, JtR, pose0, direction="inverse", _o=orig_gn):
                 out = _o(JtJ, JtR, pose0)
-                if perturb_first is not None and not log["R"]:  # the first update's translation, moved
-                    out = [out[0], out[1] + torch.from_numpy(perturb_first).to(out[1].dtype).view_as(out[1])]
+                if perturb_first is not None:  # every update moved by fresh U(+-amplitude) noise
+                    rng, amp = perturb_first
+                    dR = torch.from_numpy(rng.uniform(-amp, amp, size=tuple(out[0].shape))).to(out[0].dtype)
+                    dt = torch.from_numpy(rng.uniform(-amp, amp, size=tuple(out[1].shape))).to(out[1].dtype)
+                    out = [out[0] + dR, out[1] + dt]
                 log["jtj"].append(JtJ.detach().numpy().copy())
                 log["jtr"].append(JtR.detach().numpy().reshape(-1, 6).copy())
                 log["R"].append(out[0].detach().numpy().copy())
@@ -196,8 +203,7 @@ def add_noise_floor(torch, A, name):
     rng = np.random.default_rng(sum(ord(c) for c in name))
     Rs, ts = [], []
     for _ in range(NOISE_TRIALS):
-        jit = rng.uniform(-JITTER_ABS, JITTER_ABS, size=(len(recipe.CASES[name]["pairs"]), 3)).astype(np.float32)
-        _, res = run_case(torch, A, name, torch.float32, perturb_first=jit)
+        _, res = run_case(torch, A, name, torch.float32, perturb_first=(rng, JITTER_ABS))
         Rs.append(res["R"])
         ts.append(res["t"])
     nthreads = torch.get_num_threads()
@@ -229,8 +235,7 @@ def add_noise_floor64(torch, A, name):
     rng = np.random.default_rng(7 + sum(ord(c) for c in name))
     Rs, ts = [], []
     for _ in range(NOISE_TRIALS):
-        jit = rng.uniform(-NOISE64_ABS, NOISE64_ABS, size=(len(recipe.CASES[name]["pairs"]), 3))
-        _, res = run_case(torch, A, name, torch.float64, perturb_first=jit)
+        _, res = run_case(torch, A, name, torch.float64, perturb_first=(rng, NOISE64_ABS))
         Rs.append(res["R"])
         ts.append(res["t"])
     out["f64_jitter_R"], out["f64_jitter_t"] = np.stack(Rs), np.stack(ts)

@@ -366,13 +366,18 @@ def test_cfg4_sweep_b256():
     Rs, ts = cb.perturbed_starts(Rt, tt, rot, trs)
     assert Rs.shape[:2] == (30, B)
     Rf, tf = cb.solve_from_starts(lv, K, Rs, ts)
-    # the six zero-offset start sets are the same starts (the target itself) solved as
-    # different batches of the grouped calls (every call the same size: a short last round is
-    # padded): each pair's schedule is identical, so they must agree bit for bit -- a
-    # difference would be cross-batch interference (shared counters / extrema slots)
+    # the zero-offset start sets of the three rotation axes are the same starts (the target
+    # through an Euler round trip), those of the three translation axes the target itself,
+    # each solved as a different batch of the grouped calls (every call the same size: a short
+    # last round is padded): each pair's schedule is identical, so each group of three must
+    # agree bit for bit -- a difference would be cross-batch interference (shared counters /
+    # extrema slots)
     zero = [a * 5 + 2 for a in range(6)]
-    for zz in zero[1:]:
-        assert torch.equal(Rf[zz], Rf[zero[0]]) and torch.equal(tf[zz], tf[zero[0]]), f"start set {zz} vs {zero[0]}"
+    assert torch.equal(Rs[zero[3]], Rt) and torch.equal(ts[zero[3]], tt.reshape(B, 3))
+    for grp in (zero[:3], zero[3:]):
+        for zz in grp[1:]:
+            assert torch.equal(Rs[zz], Rs[grp[0]]) and torch.equal(ts[zz], ts[grp[0]])
+            assert torch.equal(Rf[zz], Rf[grp[0]]) and torch.equal(tf[zz], tf[grp[0]]), f"start set {zz} vs {grp[0]}"
     G = 8
     for p in (0, 13, 29):
         # grouped = one call per start set: at a common pose (the grouped solve's result) one
@@ -404,6 +409,6 @@ def test_cfg4_sweep_b256():
             assert rel <= 1e-5, f"start set {p} level {l}: JtJ grouped vs alone rel {rel:.2e}"
     counts, m = cb.basin_counts(Rf, tf, Rt, tt, rot_thresh=0.01, trans_thresh=0.01)
     near = (np.abs(m["rot_margin"]) < bound[None]) | (np.abs(m["trans_margin"]) < bound[None])
-    assert len(set(counts[zero].tolist())) == 1
+    assert len(set(counts[zero[:3]].tolist())) == 1 and len(set(counts[zero[3:]].tolist())) == 1
     print("cfg4 sweep counts (6 axes x 5 offsets):", counts.reshape(6, 5).tolist(),
           "undecided (margin < uncertainty):", near.sum(1).reshape(6, 5).tolist())

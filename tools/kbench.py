@@ -22,15 +22,21 @@ p.add_argument("--mode", choices=["reduce", "iterate", "level"], default="reduce
 p.add_argument("--c4", action="store_true", help="channel-quad packed features")
 p.add_argument("--schedule", default=None, help="auto | march | split (channel-quad reduce kernel)")
 p.add_argument("--warm-ms", type=float, default=300.0, help="warm-up time before timing")
+p.add_argument("--width", type=int, default=640,
+               help="crop every level to (width >> level) columns (strip-count experiments)")
+p.add_argument("--icp", action="store_true", help="cfg5: with the combine_ICP term (bench.py --icp)")
 p.add_argument("--from-solve", action="store_true",
                help="start from the poses of one full pyramid solve (the bench's operating point) instead of identity")
 a = p.parse_args()
 dev = torch.device("cuda:0")
-sel, levels, K = bench.make_batches(a.batch, 0, a.groups, dev)
+sel, levels, K = bench.make_batches(a.batch, 0, a.groups, dev, a.icp)
+if a.width != 640:
+    levels = [{k: v[..., : a.width >> l].contiguous() for k, v in d.items()} for l, d in enumerate(levels)]
 if a.c4:
     for d in levels:
         d["x0"], d["x1"] = ic.pack_features(d["x0"]), ic.pack_features(d["x1"])
-solver = ic.PyramidSolver(levels, K, iters=3, remove_tru_sigma=True, schedule=a.schedule, group=a.batch)
+solver = ic.PyramidSolver(levels, K, iters=3, remove_tru_sigma=True, combine_icp=a.icp,
+                         schedule=a.schedule, group=a.batch)
 R = torch.eye(3, device=dev).repeat(a.batch * a.groups, 1, 1).contiguous()
 t = torch.zeros(a.batch * a.groups, 3, device=dev)
 import ctypes
@@ -68,5 +74,5 @@ for level in ([a.level] if a.level >= 0 else range(len(solver.calls))):
     torch.cuda.synchronize()
     us = e0.elapsed_time(e1) / (a.reps * per) * 1e3
     gbs = solver.algorithmic_bytes(level) / (us * 1e-6) / 1e9
-    print(f"{os.path.basename(os.environ.get('DPFT_LIB', 'libdpft_ic.so'))}{' c4' if a.c4 else ''}{' ' + a.schedule if a.schedule else ''} {a.mode} level {level} B={a.batch}x{a.groups}: "
+    print(f"{os.path.basename(os.environ.get('DPFT_LIB', 'libdpft_ic.so'))}{' c4' if a.c4 else ''}{' icp' if a.icp else ''}{' ' + a.schedule if a.schedule else ''} {a.mode} level {level} B={a.batch}x{a.groups}: "
           f"{us:.1f} us/launch, {gbs:.0f} GB/s algorithmic ({gbs / 80:.1f}% of 8 TB/s)", flush=True)

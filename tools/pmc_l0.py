@@ -32,18 +32,18 @@ def src_sha():
     return hashlib.sha256(open(SRC, "rb").read()).hexdigest()
 
 
-def isa_sha():
+def isa_sha(kernel=None):
     """Hash of the measured kernel's machine code (deep_prob_feature_track_amd/build.py)."""
     sys.path.insert(0, ROOT)
     from deep_prob_feature_track_amd import build as B
     lib = os.environ.get("DPFT_LIB")
-    return (B.isa_hashes(os.path.abspath(lib)) if lib else json.load(open(B.ISA_OUT))).get(B.L0_KERNEL)
+    return (B.isa_hashes(os.path.abspath(lib)) if lib else json.load(open(B.ISA_OUT))).get(kernel or B.L0_KERNEL)
 
 
-def run_pass(counter, outdir, groups):
+def run_pass(counter, outdir, groups, icp=False):
     cmd = ["timeout", "-s", "KILL", "90", "rocprofv3", "--pmc", counter, "--output-format", "csv", "-d", outdir,
            "-o", "c", "--", sys.executable, os.path.join(ROOT, "tools", "kbench.py"), "--c4", "--level", "0",
-           "--mode", "level", "--from-solve", "--reps", "10", "--warm-ms", "0", "--groups", str(groups)]
+           "--mode", "level", "--from-solve", "--reps", "10", "--warm-ms", "0", "--groups", str(groups)] + (["--icp"] if icp else [])
     env = dict(os.environ, TMPDIR="/tmp")
     if env.get("DPFT_LIB"):  # a variant library (tools/build_variants.py); the profiler runs from /tmp
         env["DPFT_LIB"] = os.path.abspath(env["DPFT_LIB"])
@@ -70,6 +70,7 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--out", required=True)
     ap.add_argument("--groups", type=int, default=16, help="8-pair batches per launch (bench.py --groups)")
+    ap.add_argument("--icp", action="store_true", help="the combine_ICP kernel (bench.py --icp)")
     ap.add_argument("--from-dir", help="parse the fetch/ and write/ CSVs under this directory instead of running")
     a = ap.parse_args()
     tmp = os.path.join(ROOT, "gpurun_out", "pmc_l0")
@@ -77,12 +78,15 @@ def main():
         fetch, nf = parse("FETCH_SIZE", os.path.join(a.from_dir, "fetch"))
         write, nw = parse("WRITE_SIZE", os.path.join(a.from_dir, "write"))
     else:
-        fetch, nf = run_pass("FETCH_SIZE", os.path.join(tmp, "fetch"), a.groups)
-        write, nw = run_pass("WRITE_SIZE", os.path.join(tmp, "write"), a.groups)
-    out = {"kernel": f"ic_reduce_kernel<32,Cs=1,tru,U_IC,c4> level 0, {a.groups} x 8 pairs per launch, 640x480 "
+        fetch, nf = run_pass("FETCH_SIZE", os.path.join(tmp, "fetch"), a.groups, a.icp)
+        write, nw = run_pass("WRITE_SIZE", os.path.join(tmp, "write"), a.groups, a.icp)
+    sys.path.insert(0, ROOT)
+    from deep_prob_feature_track_amd import build as B
+    kernel = B.ICP_KERNEL if a.icp else B.L0_KERNEL
+    out = {"kernel": f"ic_reduce_kernel<32,Cs=1,tru,{'U_IC+ICP' if a.icp else 'U_IC'},c4> level 0, {a.groups} x 8 pairs per launch, 640x480 "
                      "(tools/kbench.py --mode level --from-solve)",
            "pairs_per_launch": 8 * a.groups, "group": 8,
-           "src_sha256": src_sha(), "isa_sha256": isa_sha(), "launches": {"fetch": nf, "write": nw},
+           "src_sha256": src_sha(), "isa_sha256": isa_sha(kernel), "combine_icp": a.icp, "launches": {"fetch": nf, "write": nw},
            "FETCH_SIZE_KiB": fetch, "WRITE_SIZE_KiB": write,
            "read_bytes": 2 * 1024 * fetch, "write_bytes": 1024 * write,
            "hbm_bytes": 2 * 1024 * fetch + 1024 * write,
