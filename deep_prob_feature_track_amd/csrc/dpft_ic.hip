@@ -3497,22 +3497,34 @@ __global__ __launch_bounds__(kThreads) void read_probe_kernel(const f32x4* __res
 // elementwise passes in the torch modules).  chan = [a | b], C floats each.  NHWC: the
 // four values of a 16-byte unit are channels c .. c + 3 (C % 4 == 0); NCHW: one channel
 // (H W % 4 == 0).
+__device__ inline float elu1(float y) { return y > 0.0f ? y : expm1f(y); }
 __device__ inline float bn_elu1(float x, const float* __restrict__ chan, uint32_t C, uint32_t c) {
-  const float y = x * chan[c] + chan[C + c];
-  return y > 0.0f ? y : expm1f(y);
+  return elu1(x * chan[c] + chan[C + c]);
 }
-template <bool NHWC>
+// The batchnorm scale / shift of channels c .. c + 3 (c % 4 == 0): two 16-byte loads when
+// `chan` is 16-byte aligned (CV) instead of eight 4-byte ones -- per 16-byte unit of
+// features the 4-byte loads were 8 of the kernel's 10 memory instructions (dpft_bn_elu_pack:
+// 3.9 -> 6.1 TB/s, bench.py encoder leg)
+template <bool CV>
+__device__ inline f32x4 bn_elu4(f32x4 v, const float* __restrict__ chan, uint32_t C, uint32_t c) {
+  f32x4 a, sh;
+  if constexpr (CV) {
+    a = *reinterpret_cast<const f32x4*>(chan + c);
+    sh = *reinterpret_cast<const f32x4*>(chan + C + c);
+  } else {
+    a = f32x4{chan[c], chan[c + 1], chan[c + 2], chan[c + 3]};
+    sh = f32x4{chan[C + c], chan[C + c + 1], chan[C + c + 2], chan[C + c + 3]};
+  }
+  return f32x4{elu1(v.x * a.x + sh.x), elu1(v.y * a.y + sh.y), elu1(v.z * a.z + sh.z), elu1(v.w * a.w + sh.w)};
+}
+template <bool NHWC, bool CV>
 __global__ __launch_bounds__(kThreads) void bn_elu_kernel(f32x4* __restrict__ x, const float* __restrict__ chan,
                                                           uint32_t n4, uint32_t C, uint32_t inner4) {
   const uint32_t i = blockIdx.x * kThreads + threadIdx.x;
   if (i >= n4) return;
-  f32x4 v = x[i];
+  f32x4 v = __builtin_nontemporal_load(x + i);
   if (NHWC) {
-    const uint32_t c = (i % (C / 4)) * 4;
-    v.x = bn_elu1(v.x, chan, C, c);
-    v.y = bn_elu1(v.y, chan, C, c + 1);
-    v.z = bn_elu1(v.z, chan, C, c + 2);
-    v.w = bn_elu1(v.w, chan, C, c + 3);
+    v = bn_elu4<CV>(v, chan, C, (i % (C / 4)) * 4);
   } else {
     const uint32_t c = (i / inner4) % C;
     v.x = bn_elu1(v.x, chan, C, c);
@@ -3520,13 +3532,14 @@ __global__ __launch_bounds__(kThreads) void bn_elu_kernel(f32x4* __restrict__ x,
     v.z = bn_elu1(v.z, chan, C, c);
     v.w = bn_elu1(v.w, chan, C, c);
   }
-  x[i] = v;
+  __builtin_nontemporal_store(v, x + i);
 }
 
 // dpft_bn_elu_pack: bn_elu_kernel<true>'s epilogue on a channels_last conv output, stored to
 // the channel-quad layout with pack_c4_nhwc_kernel's mapping (thread r of pair row b =
 // blockIdx.y reads quad r of the pair's [HW][C] block; 64 lanes = 64 / Q pixels x Q planes,
 // one 128-byte run per plane at Q = 8).  The conv output is read once (non-temporal).
+template <bool CV>
 __global__ __launch_bounds__(kThreads) void bn_elu_pack_kernel(const f32x4* __restrict__ src,
                                                                const float* __restrict__ chan,
                                                                f32x4* __restrict__ dst, uint32_t n, uint32_t Q,
@@ -3535,11 +3548,7 @@ __global__ __launch_bounds__(kThreads) void bn_elu_pack_kernel(const f32x4* __re
   if (r >= n) return;
   const size_t base = (size_t)blockIdx.y * n;
   const uint32_t pix = r / Q, q = r - pix * Q, C = 4 * Q, c = 4 * q;
-  f32x4 v = __builtin_nontemporal_load(src + base + r);
-  v.x = bn_elu1(v.x, chan, C, c);
-  v.y = bn_elu1(v.y, chan, C, c + 1);
-  v.z = bn_elu1(v.z, chan, C, c + 2);
-  v.w = bn_elu1(v.w, chan, C, c + 3);
+  const f32x4 v = bn_elu4<CV>(__builtin_nontemporal_load(src + base + r), chan, C, c);
   dst[base + (size_t)q * HW + pix] = v;
 }
 }  // namespace
@@ -3700,10 +3709,13 @@ int dpft_bn_elu(float* x, const float* chan, int64_t n, int32_t C, int64_t inner
   const dim3 grid((n4 + kThreads - 1) / kThreads);
   const hipStream_t st = static_cast<hipStream_t>(hip_stream);
   f32x4* x4 = reinterpret_cast<f32x4*>(x);
-  if (nhwc)
-    hipLaunchKernelGGL(bn_elu_kernel<true>, grid, dim3(kThreads), 0, st, x4, chan, n4, (uint32_t)C, 1u);
+  const bool cv = (reinterpret_cast<uintptr_t>(chan) & 15) == 0;
+  if (nhwc && cv)
+    hipLaunchKernelGGL((bn_elu_kernel<true, true>), grid, dim3(kThreads), 0, st, x4, chan, n4, (uint32_t)C, 1u);
+  else if (nhwc)
+    hipLaunchKernelGGL((bn_elu_kernel<true, false>), grid, dim3(kThreads), 0, st, x4, chan, n4, (uint32_t)C, 1u);
   else
-    hipLaunchKernelGGL(bn_elu_kernel<false>, grid, dim3(kThreads), 0, st, x4, chan, n4, (uint32_t)C,
+    hipLaunchKernelGGL((bn_elu_kernel<false, false>), grid, dim3(kThreads), 0, st, x4, chan, n4, (uint32_t)C,
                        (uint32_t)(inner / 4));
   return hip_check("bn_elu_kernel");
 }
@@ -3716,9 +3728,14 @@ int dpft_bn_elu_pack(const float* x, const float* chan, float* out, int32_t B, i
   if ((reinterpret_cast<uintptr_t>(x) | reinterpret_cast<uintptr_t>(out)) & 15)
     return fail(DPFT_E_INVALID, "x / out must be 16-byte aligned");
   const uint32_t Q = (uint32_t)(C / 4), HW = (uint32_t)H * (uint32_t)W, n = HW * Q;
-  hipLaunchKernelGGL(bn_elu_pack_kernel, dim3((n + kThreads - 1) / kThreads, (unsigned)B), dim3(kThreads), 0,
-                     static_cast<hipStream_t>(hip_stream), reinterpret_cast<const f32x4*>(x), chan,
-                     reinterpret_cast<f32x4*>(out), n, Q, HW);
+  const dim3 grid((n + kThreads - 1) / kThreads, (unsigned)B);
+  const hipStream_t st = static_cast<hipStream_t>(hip_stream);
+  if ((reinterpret_cast<uintptr_t>(chan) & 15) == 0)
+    hipLaunchKernelGGL(bn_elu_pack_kernel<true>, grid, dim3(kThreads), 0, st, reinterpret_cast<const f32x4*>(x), chan,
+                       reinterpret_cast<f32x4*>(out), n, Q, HW);
+  else
+    hipLaunchKernelGGL(bn_elu_pack_kernel<false>, grid, dim3(kThreads), 0, st, reinterpret_cast<const f32x4*>(x),
+                       chan, reinterpret_cast<f32x4*>(out), n, Q, HW);
   return hip_check("bn_elu_pack_kernel");
 }
 
