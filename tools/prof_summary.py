@@ -32,6 +32,7 @@ def main():
     a = ap.parse_args()
     rows = sorted(csv.DictReader(open(a.trace)), key=lambda r: int(r["Start_Timestamp"]))
     mm_grids = sorted({int(r["Grid_Size_X"]) for r in rows if "minmax" in r["Kernel_Name"]})
+    nrm_grids = sorted({int(r["Grid_Size_X"]) for r in rows if "icp_normals" in r["Kernel_Name"]}, reverse=True)
     top = 3  # coarsest level of the 4-level bench pyramid
     ITERS = 3
     # bench.py --inflight S replays S graphs on S side streams in the timed region; the
@@ -47,13 +48,24 @@ def main():
         st = state[sid]
         name = short(r["Kernel_Name"])
         dur = (int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e3
-        if name.startswith("minmax_levels"):
+        if name.startswith("minmax_levels") and not nrm_grids:
             # one sigma0 pre-pass for all levels opens a solve; levels then advance every
             # ITERS reduce launches (extra level-0 launches after the solve stay level 0)
             st["level"], st["n_red"] = top, 0
             if st["cur"]:
                 st["solves"].append(st["cur"])
                 st["cur"] = []
+        elif nrm_grids and name.startswith("icp_normals"):
+            # combine_ICP: each level opens with frame 1's normal map (its grid gives the
+            # level: the largest is level 0); its depth1 extrema pass (a minmax_levels_kernel
+            # per level) and the sigma0 pre-pass leave the level alone
+            st["level"] = nrm_grids.index(int(r["Grid_Size_X"]))
+            st["n_red"] = None
+            if st["level"] == top and st["cur"]:
+                st["solves"].append(st["cur"])
+                st["cur"] = []
+        elif nrm_grids and "minmax" in name:
+            pass
         elif "minmax" in name:
             # per-level sigma0 pass (older traces / solves without the pre-pass): the
             # smallest opens level 3, each later one the next finer level
@@ -73,8 +85,9 @@ def main():
             continue
         layout = "nchw" if name.endswith("false>") else "c4"
         mode = "solo" if sid == solo_stream else "side streams"
-        if name.startswith(("ic_reduce", "ic_split", "finalize", "minmax")):
-            groups[(mode, layout if not name.startswith(("finalize", "minmax")) else "-", level, name)].append(dur)
+        if name.startswith(("ic_reduce", "ic_split", "finalize", "minmax", "icp_normals")):
+            groups[(mode, layout if not name.startswith(("finalize", "minmax", "icp_normals")) else "-", level,
+                    name)].append(dur)
         st["cur"].append((int(r["Start_Timestamp"]), dur, level, name,
                           int(r["Grid_Size_X"]) // max(int(r["Workgroup_Size_X"]), 1)))
     for st in state.values():
@@ -117,10 +130,12 @@ def main():
     if a.traffic:
         t = json.load(open(a.traffic))
         out["l0_traffic"] = t
+        # algorithmic bytes per level-0 launch: 640 x 480 px x 272 B (280 with combine_ICP) per pair
+        alg = 640 * 480 * (280 if t.get("combine_icp") else 272) * t.get("pairs_per_launch", 8)
         lines += ["", "## Level-0 reduce launch: HBM traffic (separate FETCH_SIZE / WRITE_SIZE passes)\n",
                   f"read {t['read_bytes'] / 1e6:.1f} MB + write {t['write_bytes'] / 1e6:.2f} MB per launch "
-                  f"({t['correction']}); algorithmic {668467200 * t.get('pairs_per_launch', 8) / 8 / 1e6:.1f} MB "
-                  f"({t.get('pairs_per_launch', 8)} pairs) -> {t['hbm_bytes'] / (668467200 * t.get('pairs_per_launch', 8) / 8):.2f}x"]
+                  f"({t['correction']}); algorithmic {alg / 1e6:.1f} MB "
+                  f"({t.get('pairs_per_launch', 8)} pairs) -> {t['hbm_bytes'] / alg:.3f}x"]
     open(a.out + ".md", "w").write("\n".join(lines) + "\n")
     json.dump(out, open(a.out + ".json", "w"), indent=1)
     print("\n".join(lines))
