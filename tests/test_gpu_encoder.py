@@ -110,6 +110,37 @@ def test_bn_elu_pack_equals_bn_elu_then_pack(cout, H, W):
     assert torch.equal(ic.unpack_features(got), y.contiguous())
 
 
+def test_epilogue_channel_loads_aligned_and_unaligned_agree():
+    """dpft_bn_elu / dpft_bn_elu_pack load the batchnorm scale / shift of a channel quad as
+    two 16-byte words when the coefficient array is 16-byte aligned, else as eight floats:
+    both paths give the same bits (the same fused multiply-add and ELU per channel)."""
+    from deep_prob_feature_track_amd import _native as N, ic
+    dev = _dev()
+    torch.manual_seed(3)
+    B, C, H, W = 2, 16, 24, 40
+    conv = torch.randn(B, C, H, W, device=dev).contiguous(memory_format=torch.channels_last)
+    coeffs = torch.cat((torch.rand(C, device=dev) + 0.5, torch.randn(C, device=dev) * 0.3))
+    store = torch.zeros(2 * C + 4, device=dev)
+    store[1:1 + 2 * C] = coeffs
+    aligned, unaligned = coeffs.contiguous(), store[1:1 + 2 * C]
+    assert aligned.data_ptr() % 16 == 0 and unaligned.data_ptr() % 16 != 0
+    L = N.lib()
+    outs = []
+    for chan in (aligned, unaligned):
+        packed = torch.empty(B, C // 4, H, W, 4, device=dev)
+        N.check(L.dpft_bn_elu_pack(ic._ptr(conv), ic._ptr(chan), ic._ptr(packed), B, C, H, W, ic._stream(dev)),
+                "dpft_bn_elu_pack")
+        inplace = conv.clone(memory_format=torch.channels_last)
+        N.check(L.dpft_bn_elu(ic._ptr(inplace), ic._ptr(chan), inplace.numel(), C, 1, 1, ic._stream(dev)),
+                "dpft_bn_elu")
+        outs.append((packed, inplace))
+    torch.cuda.synchronize()
+    assert torch.equal(outs[0][0], outs[1][0]) and torch.equal(outs[0][1], outs[1][1])
+    assert torch.equal(ic.pack_features(outs[0][1]), outs[0][0])
+    ref = torch.nn.functional.elu(conv * coeffs[:C].view(1, C, 1, 1) + coeffs[C:].view(1, C, 1, 1))
+    torch.testing.assert_close(outs[0][1], ref, rtol=1e-6, atol=1e-6)
+
+
 def test_dropin_encoder_writes_packed_features():
     """LeastSquareTracking's feature heads write the solver's channel-quad layout (no
     relayout pass in the forward): the packed features are bit for bit the heads' conv
