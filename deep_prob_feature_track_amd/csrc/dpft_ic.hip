@@ -591,33 +591,61 @@ struct IcpTerm {
   bool occ;
 };
 
-__device__ __forceinline__ IcpTerm icp_pixel(float xr, float yr, float d0, const float* __restrict__ Rm,
-                                             const float* __restrict__ tv, float fx, float fy, float cx, float cy,
-                                             int H, int W, const f32x4* __restrict__ nd1, bool mask0_bg,
-                                             const uint8_t* __restrict__ m1b, float wgt) {
-#pragma clang fp contract(off)
-  // vertex0 = [px, py, 1] * depth0; P = R V0 + t (CPU bmm order, then + t)
-  const float V0x = xr * d0, V0y = yr * d0, V0z = d0;
-  const float Px = __builtin_fmaf(Rm[2], V0z, __builtin_fmaf(Rm[1], V0y, Rm[0] * V0x)) + tv[0];
-  const float Py = __builtin_fmaf(Rm[5], V0z, __builtin_fmaf(Rm[4], V0y, Rm[3] * V0x)) + tv[1];
-  const float Pz = __builtin_fmaf(Rm[8], V0z, __builtin_fmaf(Rm[7], V0y, Rm[6] * V0x)) + tv[2];
-  const float u = (Px / Pz) * fx + cx;
-  const float v = (Py / Pz) * fy + cy;
-  const bool inview = (u > 0.0f) && (u < (float)(W - 1)) && (v > 0.0f) && (v < (float)(H - 1));
+// The term in three parts, so that the marching kernel can issue the normal-map taps before
+// the pixel's IC normal-equation update and consume them after it (that arithmetic then
+// covers part of the loads' latency): icp_geo (projection, in-view test, taps: pose and
+// depth0 only), icp_load (the four tap loads), icp_term (the rest).
+struct IcpGeo {
+  float V0x, V0y, V0z, Px, Py, Pz;
+  bool inview;
+  Taps tp;
   int x0, x1, y0, y1;
-  const Taps tp = make_taps_xy(u, v, H, W, x0, x1, y0, y1);
+};
+struct IcpTaps {
+  f32x4 q00, q01, q10, q11;
+};
+
+__device__ __forceinline__ IcpGeo icp_geo(float xr, float yr, float d0, const float* __restrict__ Rm,
+                                          const float* __restrict__ tv, float fx, float fy, float cx, float cy, int H,
+                                          int W) {
+#pragma clang fp contract(off)
+  IcpGeo g;
+  // vertex0 = [px, py, 1] * depth0; P = R V0 + t (CPU bmm order, then + t)
+  g.V0x = xr * d0;
+  g.V0y = yr * d0;
+  g.V0z = d0;
+  g.Px = __builtin_fmaf(Rm[2], g.V0z, __builtin_fmaf(Rm[1], g.V0y, Rm[0] * g.V0x)) + tv[0];
+  g.Py = __builtin_fmaf(Rm[5], g.V0z, __builtin_fmaf(Rm[4], g.V0y, Rm[3] * g.V0x)) + tv[1];
+  g.Pz = __builtin_fmaf(Rm[8], g.V0z, __builtin_fmaf(Rm[7], g.V0y, Rm[6] * g.V0x)) + tv[2];
+  const float u = (g.Px / g.Pz) * fx + cx;
+  const float v = (g.Py / g.Pz) * fy + cy;
+  g.inview = (u > 0.0f) && (u < (float)(W - 1)) && (v > 0.0f) && (v < (float)(H - 1));
+  // (the taps are clamped into the image whatever u, v are -- NaN included -- so the loads
+  // below stay in bounds on every lane)
+  g.tp = make_taps_xy(u, v, H, W, g.x0, g.x1, g.y0, g.y1);
+  return g;
+}
+
+__device__ __forceinline__ IcpTaps icp_load(const IcpGeo& g, const f32x4* __restrict__ nd1) {
+  return IcpTaps{nd1[g.tp.o00], nd1[g.tp.o01], nd1[g.tp.o10], nd1[g.tp.o11]};
+}
+
+__device__ __forceinline__ IcpTerm icp_term(const IcpGeo& g, const IcpTaps& q, float d0,
+                                            const float* __restrict__ Rm, float fx, float fy, float cx, float cy,
+                                            bool mask0_bg, const uint8_t* __restrict__ m1b, float wgt) {
+#pragma clang fp contract(off)
+  const Taps& tp = g.tp;
   // vertex1 sampled: the vertex map at the four taps, then the sampler's chain
-  const f32x4 q00 = nd1[tp.o00], q01 = nd1[tp.o01], q10 = nd1[tp.o10], q11 = nd1[tp.o11];
-  const float a = q00.w, b = q01.w, c = q10.w, d = q11.w;
-  const float px0 = ((float)x0 - cx) / fx, px1 = ((float)x1 - cx) / fx;
-  const float py0 = ((float)y0 - cy) / fy, py1 = ((float)y1 - cy) / fy;
+  const float a = q.q00.w, b = q.q01.w, c = q.q10.w, d = q.q11.w;
+  const float px0 = ((float)g.x0 - cx) / fx, px1 = ((float)g.x1 - cx) / fx;
+  const float py0 = ((float)g.y0 - cy) / fy, py1 = ((float)g.y1 - cy) / fy;
   const float V1x = bil4(px0 * a, px1 * b, px0 * c, px1 * d, tp);
   const float V1y = bil4(py0 * a, py0 * b, py1 * c, py1 * d, tp);
   const float V1z = bil4(a, b, c, d, tp);
-  const float Nx = bil4(q00.x, q01.x, q10.x, q11.x, tp), Ny = bil4(q00.y, q01.y, q10.y, q11.y, tp);
-  const float Nz = bil4(q00.z, q01.z, q10.z, q11.z, tp);
-  const float Dx = Px - V1x, Dy = Py - V1y, Dz = Pz - V1z;
-  bool occ = !inview || (sqrtf((Dx * Dx + Dy * Dy) + Dz * Dz) > 0.1f) || mask0_bg;
+  const float Nx = bil4(q.q00.x, q.q01.x, q.q10.x, q.q11.x, tp), Ny = bil4(q.q00.y, q.q01.y, q.q10.y, q.q11.y, tp);
+  const float Nz = bil4(q.q00.z, q.q01.z, q.q10.z, q.q11.z, tp);
+  const float Dx = g.Px - V1x, Dy = g.Py - V1y, Dz = g.Pz - V1z;
+  bool occ = !g.inview || (sqrtf((Dx * Dx + Dy * Dy) + Dz * Dz) > 0.1f) || mask0_bg;
   if (m1b) occ = occ || !(bil_u8(m1b, tp) > 0.0f);
   float r = (Nx * Dx + Ny * Dy) + Nz * Dz;
   // n = N1w^T R ; J = [n x V0, -n]
@@ -639,15 +667,23 @@ __device__ __forceinline__ IcpTerm icp_pixel(float xr, float yr, float d0, const
   // (1 ulp each, no IEEE division / sqrt sequences): continuous weights only
   const float rsig = wgt * __builtin_amdgcn_rcpf(__builtin_amdgcn_sqrtf(cov + 1e-8f) + 1e-8f);
   IcpTerm o;
-  o.J[0] = (n2 * V0y - n1 * V0z) * rsig;
-  o.J[1] = (n0 * V0z - n2 * V0x) * rsig;
-  o.J[2] = (n1 * V0x - n0 * V0y) * rsig;
+  o.J[0] = (n2 * g.V0y - n1 * g.V0z) * rsig;
+  o.J[1] = (n0 * g.V0z - n2 * g.V0x) * rsig;
+  o.J[2] = (n1 * g.V0x - n0 * g.V0y) * rsig;
   o.J[3] = n0 * rsig;
   o.J[4] = n1 * rsig;
   o.J[5] = n2 * rsig;
   o.r = occ ? 1e-6f * wgt : r * rsig;
   o.occ = occ;
   return o;
+}
+
+__device__ __forceinline__ IcpTerm icp_pixel(float xr, float yr, float d0, const float* __restrict__ Rm,
+                                             const float* __restrict__ tv, float fx, float fy, float cx, float cy,
+                                             int H, int W, const f32x4* __restrict__ nd1, bool mask0_bg,
+                                             const uint8_t* __restrict__ m1b, float wgt) {
+  const IcpGeo g = icp_geo(xr, yr, d0, Rm, tv, fx, fy, cx, cy, H, W);
+  return icp_term(g, icp_load(g, nd1), d0, Rm, fx, fy, cx, cy, mask0_bg, m1b, wgt);
 }
 
 // Frame-1 normal map of one level (algorithms.py:2148-2172): vertex map
@@ -1258,7 +1294,9 @@ __global__ __launch_bounds__(kThreads, 1) void ic_reduce_kernel(IterParams p) {
   struct Sums {
     float Saa[R], Sab[R], Sbb[R], Sa[R], Sb[R], Sar[R], Sbr[R];
   };
-  auto finish_pixels = [&](const Frame& F, const PixelTerms& T, Sums& S) {
+  // d0q (combine_ICP, R == 1): depth0 of the pixel, loaded by the caller before the
+  // pixel's epilogue (the marching path); null: loaded here
+  auto finish_pixels = [&](const Frame& F, const PixelTerms& T, Sums& S, const float* d0q = nullptr) {
 #pragma unroll
     for (int r = 0; r < R; ++r) {
       if (!F.out_lane || F.y0 + r >= H) continue;
@@ -1268,6 +1306,16 @@ __global__ __launch_bounds__(kThreads, 1) void ic_reduce_kernel(IterParams p) {
       const float Sa = -S.Sa[r] * wp, Sb = -S.Sb[r] * wp, Sar = -S.Sar[r] * wp, Sbr = -S.Sbr[r] * wp;
       const float Saa = S.Saa[r] * wp, Sab = S.Sab[r] * wp, Sbb = S.Sbb[r] * wp;
       const bool invalid = T.invalid[r];
+      // combine_ICP: the point-to-plane term's geometry and its four normal-map taps first,
+      // so that the IC update below runs while they load
+      IcpGeo icg{};
+      IcpTaps icq{};
+      float d0v = 0.f;
+      if constexpr (ICP) {
+        d0v = (R == 1 && d0q) ? *d0q : p.depth0[(size_t)b * HW + (F.y0 + r) * W + F.xc];
+        icg = icp_geo(F.wp[r].xr, F.wp[r].yr, d0v, Rm, tv, fx, fy, cx, cy, H, W);
+        icq = icp_load(icg, p.nrm1 + (size_t)b * HW);
+      }
       float Jx[6], Jy[6];
       warp_jac(F.wp[r].xr, F.wp[r].yr, F.d[r], fx, fy, Jx, Jy);
       // weighted residual of invalid pixels is 1e-6 on every channel (algorithms.py:1982-1983)
@@ -1292,10 +1340,7 @@ __global__ __launch_bounds__(kThreads, 1) void ic_reduce_kernel(IterParams p) {
       for (int i = 0; i < 6; ++i) acc[21 + i] -= cA * Jx[i] + cB * Jy[i];
       ninv += invalid ? 1.0f : 0.0f;
       if (ICP) {  // JtWJ += (wJ)^T (wJ), JtR += (wJ)^T (w r)  (algorithms.py:668-689)
-        const int yr = F.y0 + r;
-        const float d0v = p.depth0[(size_t)b * HW + yr * W + F.xc];
-        const IcpTerm ic = icp_pixel(F.wp[r].xr, F.wp[r].yr, d0v, Rm, tv, fx, fy, cx, cy, H, W,
-                                     p.nrm1 + (size_t)b * HW, !F.m0[r], m1b, p.icp_w);
+        const IcpTerm ic = icp_term(icg, icq, d0v, Rm, fx, fy, cx, cy, !F.m0[r], m1b, p.icp_w);
         int kq2 = 0;
 #pragma unroll
         for (int i = 0; i < 6; ++i) {
@@ -1710,6 +1755,9 @@ __global__ __launch_bounds__(kThreads, 1) void ic_reduce_kernel(IterParams p) {
         }
         unitc(qq, L[qq % RM]);
       }
+      // combine_ICP: the pixel's depth0, loaded here (after the channel loop: no register
+      // across it) so that the sigma / pixel terms below run while it loads
+      const float d0e = ICP ? p.depth0[(size_t)b * HW + y * W + min(max(xs, 0), W - 1)] : 0.f;
       // the frame's gathers and the sigma0 row are resolved after the channel loop (a
       // select of a loaded value under the wave-uniform direction becomes a branch whose
       // copies wait for every load in flight, before the first tap is issued)
@@ -1738,7 +1786,7 @@ __global__ __launch_bounds__(kThreads, 1) void ic_reduce_kernel(IterParams p) {
       S.Sb[0] = A * q[7] + by * q[8];
       S.Sar[0] = A2 * q[3] + A * bx * q[5];
       S.Sbr[0] = A2 * q[4] + A * by * q[5];
-      finish_pixels(F, T, S);
+      finish_pixels(F, T, S, &d0e);
     };
     for (int k = 0; k < nrows; ++k) step(k);
   } else if constexpr (C4) {
