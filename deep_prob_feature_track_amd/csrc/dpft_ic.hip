@@ -645,7 +645,11 @@ __device__ __forceinline__ IcpTerm icp_term(const IcpGeo& g, const IcpTaps& q, f
   const float Nx = bil4(q.q00.x, q.q01.x, q.q10.x, q.q11.x, tp), Ny = bil4(q.q00.y, q.q01.y, q.q10.y, q.q11.y, tp);
   const float Nz = bil4(q.q00.z, q.q01.z, q.q10.z, q.q11.z, tp);
   const float Dx = g.Px - V1x, Dy = g.Py - V1y, Dz = g.Pz - V1z;
-  bool occ = !g.inview || (sqrtf((Dx * Dx + Dy * Dy) + Dz * Dz) > 0.1f) || mask0_bg;
+  // ||diff|| > 0.1 (936-940) as a test of the squared norm against the largest float whose
+  // correctly rounded square root is <= 0.1f (0x3c23d70b): sqrt is monotonic, so the two tests
+  // agree on every input (checked exhaustively around the threshold), without the IEEE
+  // square-root sequence
+  bool occ = !g.inview || ((Dx * Dx + Dy * Dy) + Dz * Dz > __uint_as_float(0x3c23d70bu)) || mask0_bg;
   if (m1b) occ = occ || !(bil_u8(m1b, tp) > 0.0f);
   float r = (Nx * Dx + Ny * Dy) + Nz * Dz;
   // n = N1w^T R ; J = [n x V0, -n]
@@ -1282,8 +1286,10 @@ __global__ __launch_bounds__(kThreads, 1) void ic_reduce_kernel(IterParams p) {
         T.sr0[r] = bilp(F.gs1[r], F.pw[r]);
         T.srmin[r] = T.srmax[r] = T.sr0[r];
         const float s0m = F.s0r[r + 1];
-        const float sg = sqrtf(T.sr0[r] * T.sr0[r] + s0m * s0m);
-        T.inv_s[r] = __builtin_amdgcn_rcpf(sg);  // 1 ulp; r * (1/sigma) is a continuous weight
+        // sigma and 1 / sigma by the hardware square root and reciprocal (1 ulp each; only
+        // continuous weights depend on them, no test does)
+        const float sg = __builtin_amdgcn_sqrtf(T.sr0[r] * T.sr0[r] + s0m * s0m);
+        T.inv_s[r] = __builtin_amdgcn_rcpf(sg);
         T.kk[r] = s0m * (T.inv_s[r] * T.inv_s[r] * T.inv_s[r]);
         if (TRU) T.invalid[r] = T.invalid[r] || (s0m == g0min) || (s0m == g0max);
       }
@@ -2356,7 +2362,7 @@ __device__ __forceinline__ void split_pass(const IterParams& p, int b, int jb, i
       float hx, hy;
       sobel_cols(s0t, s0m, s0b, hx, hy);
       sr0 = bilp(gs1, pw);
-      const float sg = sqrtf(sr0 * sr0 + s0m * s0m);
+      const float sg = __builtin_amdgcn_sqrtf(sr0 * sr0 + s0m * s0m);  // as pixel_terms: continuous only
       A = __builtin_amdgcn_rcpf(sg);
       const float kk = s0m * (A * A * A);
       bx = kk * hx;
