@@ -112,7 +112,7 @@ def make_batches(B, first, count, device, icp=False):
     return sel, levels, K
 
 
-def l0_traffic(pairs, group, kernel):
+def l0_traffic(pairs, group, kernel, icp=False):
     """Per-launch HBM bytes of the level-0 reduce launch from the committed PMC measurement
     (tools/pmc_l0.py: separate FETCH_SIZE / WRITE_SIZE rocprofv3 passes, gfx950-corrected),
     used only if it was measured on the machine code of the kernel built here (the ISA hash
@@ -124,7 +124,8 @@ def l0_traffic(pairs, group, kernel):
         return None
     for f in sorted(glob.glob(os.path.join(ROOT, "profiles", "*_l0_traffic.json")), reverse=True):
         d = json.load(open(f))
-        if d.get("pairs_per_launch", 8) == pairs and d.get("group", pairs) == group and d.get("isa_sha256") == isa:
+        if (d.get("pairs_per_launch", 8) == pairs and d.get("group", pairs) == group and d.get("isa_sha256") == isa
+                and bool(d.get("combine_icp", False)) == icp):
             return {"hbm_bytes": d["hbm_bytes"], "source": os.path.relpath(f, ROOT)}
     return None
 
@@ -532,9 +533,10 @@ def main():
     kern_us = _timed(l0, groups, device) / len(l0_group) * 1e6
     alg_bytes = solver.algorithmic_bytes(0)
     achieved = alg_bytes / (kern_us * 1e-6) / 1e9
-    mode = 1 if a.icp else 0
-    kname = f"_ZN12_GLOBAL__N_116ic_reduce_kernelILi32ELb1ELb1ELi{mode}ELb1EEEvNS_10IterParamsE"
-    traffic = l0_traffic(n_call, B, kname) if a.layout == "c4" else None
+    # (combine_ICP on the channel-quad path: the same U_IC reduce kernel plus its own ICP pass,
+    # whose bytes the --icp traffic measurement includes)
+    kname = "_ZN12_GLOBAL__N_116ic_reduce_kernelILi32ELb1ELb1ELi0ELb1EEEvNS_10IterParamsE"
+    traffic = l0_traffic(n_call, B, kname, a.icp) if a.layout == "c4" else None
     copy_gbs = copy_peak_gbs(device) if rank == 0 else None
     read_gbs = read_peak_gbs(device, alg_bytes) if rank == 0 else None
 
@@ -583,8 +585,11 @@ def main():
                          "frac": achieved / HBM_PEAK_GBS,
                          "traffic": traffic["hbm_bytes"] if traffic else None,
                          "traffic_source": traffic["source"] if traffic else None,
-                         "kernel": f"ic_reduce_kernel<32,Cs=1,tru,{'U_IC+ICP' if a.icp else 'U_IC'},{a.layout}> "
-                                   f"(level 0, {n_call} pairs per launch, + in-kernel finalize)",
+                         "kernel": (f"icp_records_kernel + ic_reduce_kernel<32,Cs=1,tru,U_IC,{a.layout}> (level 0, "
+                                    f"{n_call} pairs per launch: the combine_ICP pass, then the reduce launch with the "
+                                    f"in-kernel finalize adding its records)" if a.icp and a.layout == "c4" else
+                                    f"ic_reduce_kernel<32,Cs=1,tru,{'U_IC+ICP' if a.icp else 'U_IC'},{a.layout}> "
+                                    f"(level 0, {n_call} pairs per launch, + in-kernel finalize)"),
                          "kernel_us": kern_us, "algorithmic_bytes_per_launch": alg_bytes,
                          "algorithmic_bytes_per_pixel": bpa,
                          "measured_copy_peak": copy_gbs,

@@ -87,6 +87,9 @@ constexpr int kGridWaste = DPFT_GRID_WASTE;  // marching band grid: idle waves a
 
 // ---- reduce-record layout (floats) ------------------------------------------
 constexpr int kRec = 48;
+constexpr int kIcpRec = 32;  // icp_records_kernel record: JtJ (21) + JtR (6) + 0 (the invalid count's slot), padded
+constexpr int kIcpSub = 4;   // icp_records_kernel: at most this many workgroups (records) per reduce workgroup slot
+constexpr int kIcpTab = 2048;  // icp_records_kernel: normalised-coordinate table in LDS when W + H fits
 constexpr int R_NINV = 27;    // invalid pixels (occlusion | masks | sigma0-trunc)
 constexpr int R_MN_ALL = 28;  // min of sigma_r over every channel
 constexpr int R_MN0 = 29;     // min of sigma_r channel 0
@@ -340,6 +343,9 @@ __device__ __forceinline__ Warp warp_point(int x, int y, float d, const float* _
 // Last-block finalize parameters (one record per workgroup, fixed-order fp64 sums).
 struct FinParams {
   const float* rec;
+  const float* icp_rec;  // combine_ICP on the channel-quad path: [B][nbpp][icp_sub][kIcpRec] records of
+                         // icp_records_kernel (JtJ 21 + JtR 6), added to the reduce records; null: none
+  int icp_sub;           // icp_records_kernel workgroups per reduce workgroup slot (1 .. kIcpSub)
   int nbpp, B;        // reduce kernel: workgroups (records) per pair, pairs
   double* prec;       // [B][kPRec] per-pair records
   uint32_t* pair_cnt; // [B] completion counters
@@ -370,6 +376,7 @@ struct IterParams {
   const float* depth0;   // COMBINE_ICP: raw depth pyramids level (max-pooled), [B,1,H,W]
   const float* depth1;
   const f32x4* nrm1;     // COMBINE_ICP: frame 1's [nx, ny, nz, depth1] map, [B,H,W] (workspace, per level)
+  float* icp_rec;        // COMBINE_ICP: icp_records_kernel's records (workspace)
   float icp_w;           // ScaleNet('None') weight (algorithms.py:1563)
   const float* K;
   const float* R;
@@ -630,15 +637,24 @@ __device__ __forceinline__ IcpTaps icp_load(const IcpGeo& g, const f32x4* __rest
   return IcpTaps{nd1[g.tp.o00], nd1[g.tp.o01], nd1[g.tp.o10], nd1[g.tp.o11]};
 }
 
-__device__ __forceinline__ IcpTerm icp_term(const IcpGeo& g, const IcpTaps& q, float d0,
-                                            const float* __restrict__ Rm, float fx, float fy, float cx, float cy,
-                                            bool mask0_bg, const uint8_t* __restrict__ m1b, float wgt) {
+// The tap vertices' normalised coordinates (x - cx) / fx of the tap columns x0, x1 and
+// (y - cy) / fy of the rows y0, y1 (geometry.py:1129-1136 on the tap pixels).
+struct IcpTapXY {
+  float px0, px1, py0, py1;
+};
+__device__ __forceinline__ IcpTapXY icp_tap_xy(const IcpGeo& g, float fx, float fy, float cx, float cy) {
+#pragma clang fp contract(off)
+  return IcpTapXY{((float)g.x0 - cx) / fx, ((float)g.x1 - cx) / fx, ((float)g.y0 - cy) / fy, ((float)g.y1 - cy) / fy};
+}
+
+__device__ __forceinline__ IcpTerm icp_term(const IcpGeo& g, const IcpTaps& q, const IcpTapXY& n, float d0,
+                                            const float* __restrict__ Rm, bool mask0_bg,
+                                            const uint8_t* __restrict__ m1b, float wgt) {
 #pragma clang fp contract(off)
   const Taps& tp = g.tp;
   // vertex1 sampled: the vertex map at the four taps, then the sampler's chain
   const float a = q.q00.w, b = q.q01.w, c = q.q10.w, d = q.q11.w;
-  const float px0 = ((float)g.x0 - cx) / fx, px1 = ((float)g.x1 - cx) / fx;
-  const float py0 = ((float)g.y0 - cy) / fy, py1 = ((float)g.y1 - cy) / fy;
+  const float px0 = n.px0, px1 = n.px1, py0 = n.py0, py1 = n.py1;
   const float V1x = bil4(px0 * a, px1 * b, px0 * c, px1 * d, tp);
   const float V1y = bil4(py0 * a, py0 * b, py1 * c, py1 * d, tp);
   const float V1z = bil4(a, b, c, d, tp);
@@ -687,7 +703,7 @@ __device__ __forceinline__ IcpTerm icp_pixel(float xr, float yr, float d0, const
                                              int H, int W, const f32x4* __restrict__ nd1, bool mask0_bg,
                                              const uint8_t* __restrict__ m1b, float wgt) {
   const IcpGeo g = icp_geo(xr, yr, d0, Rm, tv, fx, fy, cx, cy, H, W);
-  return icp_term(g, icp_load(g, nd1), d0, Rm, fx, fy, cx, cy, mask0_bg, m1b, wgt);
+  return icp_term(g, icp_load(g, nd1), icp_tap_xy(g, fx, fy, cx, cy), d0, Rm, mask0_bg, m1b, wgt);
 }
 
 // Frame-1 normal map of one level (algorithms.py:2148-2172): vertex map
@@ -728,6 +744,81 @@ __global__ __launch_bounds__(kThreads) void icp_normals_kernel(const float* __re
   const float d = db[pix];
   const bool bad = d == dec_ord(dext[0]) || d == dec_ord(dext[1]);
   nrm[i] = bad ? f32x4{0.0f, 0.0f, 0.0f, d} : f32x4{n[0] / mag, n[1] / mag, n[2] / mag, d};
+}
+
+// combine_ICP on the channel-quad path: the point-to-plane term's normal equations in a pass
+// of their own (algorithms.py:916-997, 668-689), kIcpSub records per reduce workgroup slot
+// (the reduce launch's B x nbpp), which pair_reduce2 adds to that slot's reduce record:
+// workgroup (jb, u) of pair b takes pixels [HW s / (nbpp S), HW (s + 1) / (nbpp S)),
+// s = jb S + u.  S workgroups per slot (p.fin.icp_sub, up to kIcpSub where a level has the
+// pixels for it): at level 0 one workgroup per slot leaves two waves per SIMD, latency-bound
+// (252 us per 64-pair launch; four: ...).  The term needs no feature
+// bytes (depth0, the normal map's taps, the masks: 8 B per pixel of HBM plus cached taps), so
+// the reduce launch keeps the U_IC kernel's registers -- the cross-row prefetch and the ring
+// depth of the fused ICP kernel did not fit two waves per SIMD.  The
+// pixel's normalised coordinates are the marching kernel's (norm_coord: the same IEEE
+// operations), its contribution the fused kernel's (same icp_pixel, same weight); only the
+// fp32 summation grouping differs.
+__global__ __launch_bounds__(kThreads) void icp_records_kernel(IterParams p, float* __restrict__ out) {
+  __shared__ float red[4][28];
+  __shared__ float nxy[kIcpTab];  // (x - cx) / fx of the W columns, then (y - cy) / fy of the H rows
+  const int kb = blockIdx.x, nsub = p.nbpp * p.fin.icp_sub, b = kb / nsub, sb = kb - b * nsub;
+  const int W = p.W, H = p.H, HW = H * W;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const float fx = p.K[4 * b + 0], fy = p.K[4 * b + 1], cx = p.K[4 * b + 2], cy = p.K[4 * b + 3];
+  float Rm[9], tv[3];
+#pragma unroll
+  for (int k = 0; k < 9; ++k) Rm[k] = p.R[9 * b + k];
+#pragma unroll
+  for (int k = 0; k < 3; ++k) tv[k] = p.t[3 * b + k];
+  // the pair's normalised coordinates once per workgroup (the same IEEE operations as
+  // norm_coord: the same bits), read for the pixel and for its four tap vertices
+  const bool tab = W + H <= kIcpTab;
+  if (tab) {
+    for (int j = tid; j < W + H; j += kThreads) nxy[j] = j < W ? norm_coord(j, cx, fx) : norm_coord(j - W, cy, fy);
+    __syncthreads();
+  }
+  auto ncx = [&](int x) { return tab ? nxy[x] : norm_coord(x, cx, fx); };
+  auto ncy = [&](int y) { return tab ? nxy[W + y] : norm_coord(y, cy, fy); };
+  const float* d0b = p.depth0 + (size_t)b * HW;
+  const uint8_t* m0b = p.mask0 ? p.mask0 + (size_t)b * HW : nullptr;
+  const uint8_t* m1b = p.mask1 ? p.mask1 + (size_t)b * HW : nullptr;
+  const f32x4* nd1 = p.nrm1 + (size_t)b * HW;
+  const int beg = (int)(((long)HW * sb) / nsub), end = (int)(((long)HW * (sb + 1)) / nsub);
+  float acc[27];
+#pragma unroll
+  for (int i = 0; i < 27; ++i) acc[i] = 0.f;
+  int pix = beg + tid, y = pix / W, x = pix - y * W;  // then advanced by kThreads without a division
+  for (; pix < end; pix += kThreads) {
+    const bool m0 = m0b ? (m0b[pix] != 0) : true;
+    const float d0 = d0b[pix];
+    const IcpGeo g = icp_geo(ncx(x), ncy(y), d0, Rm, tv, fx, fy, cx, cy, H, W);
+    const IcpTapXY n{ncx(g.x0), ncx(g.x1), ncy(g.y0), ncy(g.y1)};
+    const IcpTerm ic = icp_term(g, icp_load(g, nd1), n, d0, Rm, !m0, m1b, p.icp_w);
+    int kq = 0;
+#pragma unroll
+    for (int i = 0; i < 6; ++i) {
+#pragma unroll
+      for (int j = i; j < 6; ++j) acc[kq++] += ic.J[i] * ic.J[j];
+    }
+#pragma unroll
+    for (int i = 0; i < 6; ++i) acc[21 + i] += ic.J[i] * ic.r;
+    x += kThreads;
+    while (x >= W) {
+      x -= W;
+      ++y;
+    }
+  }
+  // fixed-order reduction: wave butterflies, then the four waves in order
+#pragma unroll
+  for (int i = 0; i < 27; ++i) {
+    float v = acc[i];
+    for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off);
+    if (lane == 0) red[wave][i] = v;
+  }
+  __syncthreads();
+  if (tid < kIcpRec)
+    out[(size_t)kb * kIcpRec + tid] = tid < 27 ? ((red[0][tid] + red[1][tid]) + red[2][tid]) + red[3][tid] : 0.f;
 }
 
 // ============================================================ last-block finalize
@@ -1005,10 +1096,18 @@ __device__ void pair_reduce2(const FinParams& q, int b, float* sc) {
   for (int i = 0; i < 48; ++i) f[i] = 0.f;
   f[R_MN_ALL] = f[R_MN0] = INFINITY;
   f[R_MX_ALL] = f[R_MX0] = -INFINITY;
+  const int ns = q.icp_sub;
+  const Rsrc ri = rsrc(q.icp_rec ? q.icp_rec + (size_t)b * n * ns * kIcpRec : q.rec,
+                       q.icp_rec ? (uint32_t)((size_t)n * ns * kIcpRec * sizeof(float)) : 0u);
   for (int k = tid; k < n; k += kThreads) {
     f32x4 v[12];
 #pragma unroll
     for (int j = 0; j < 12; ++j) v[j] = llvm_buf_load_f32x4(rr, k * kRec * 4 + 16 * j, 0, kAuxSc1);
+    if (q.icp_rec) {  // the point-to-plane term's normal equations of the same record slot
+      for (int u = 0; u < ns; ++u)
+#pragma unroll
+        for (int j = 0; j < 7; ++j) v[j] += llvm_buf_load_f32x4(ri, (k * ns + u) * kIcpRec * 4 + 16 * j, 0, kAuxSc1);
+    }
     const float* g = reinterpret_cast<const float*>(v);
     if (k == tid) {
 #pragma unroll
@@ -1346,7 +1445,7 @@ __global__ __launch_bounds__(kThreads, 1) void ic_reduce_kernel(IterParams p) {
       for (int i = 0; i < 6; ++i) acc[21 + i] -= cA * Jx[i] + cB * Jy[i];
       ninv += invalid ? 1.0f : 0.0f;
       if (ICP) {  // JtWJ += (wJ)^T (wJ), JtR += (wJ)^T (w r)  (algorithms.py:668-689)
-        const IcpTerm ic = icp_term(icg, icq, d0v, Rm, fx, fy, cx, cy, !F.m0[r], m1b, p.icp_w);
+        const IcpTerm ic = icp_term(icg, icq, icp_tap_xy(icg, fx, fy, cx, cy), d0v, Rm, !F.m0[r], m1b, p.icp_w);
         int kq2 = 0;
 #pragma unroll
         for (int i = 0; i < 6; ++i) {
@@ -2862,10 +2961,17 @@ size_t rec_bytes(const DpftLevelDesc& d) {
   return (slots * kRec * sizeof(float) + 255) & ~(size_t)255;
 }
 
-// COMBINE_ICP: frame-1 normal + depth map [B,H,W,4] between the pair records and the
-// workgroup records (the latter grow with the number of poses of a residual call)
+// COMBINE_ICP: frame-1 normal + depth map [B,H,W,4] and the ICP records between the pair
+// records and the workgroup records (the latter grow with the number of poses of a residual
+// call)
 size_t nrm_bytes(const DpftLevelDesc& d) {
-  return (d.flags & DPFT_COMBINE_ICP) ? (size_t)d.B * 4 * d.H * d.W * sizeof(float) : 0;
+  if (!(d.flags & DPFT_COMBINE_ICP)) return 0;
+  // the map, then the ICP records (icp_records_kernel: one per reduce workgroup slot)
+  const size_t slots = std::max<size_t>(kMaxGrid, d.B);
+  return (((size_t)d.B * 4 * d.H * d.W * sizeof(float) + 255) & ~(size_t)255) + slots * kIcpSub * kIcpRec * sizeof(float);
+}
+size_t icp_rec_offset(const DpftLevelDesc& d) {
+  return kCtrlBytes + prec_bytes(d) + (((size_t)d.B * 4 * d.H * d.W * sizeof(float) + 255) & ~(size_t)255);
 }
 
 size_t ws_need(const DpftLevelDesc& d) {
@@ -2897,6 +3003,8 @@ IterParams make_params(const DpftLevelDesc& d, const DpftLevelTensors& tt, const
   p.depth1 = tt.depth1;
   p.nrm1 = (d.flags & DPFT_COMBINE_ICP) ? reinterpret_cast<const f32x4*>(static_cast<char*>(ws) + nrm_offset(d))
                                         : nullptr;
+  p.icp_rec = (d.flags & DPFT_COMBINE_ICP) ? reinterpret_cast<float*>(static_cast<char*>(ws) + icp_rec_offset(d))
+                                           : nullptr;
   p.icp_w = d.icp_weight;
   p.K = tt.K;
   p.R = R;
@@ -3022,8 +3130,18 @@ int resident_blocks(const void* kernel, int threads = kThreads) {
   return n;
 }
 
+// combine_ICP through its own pass: the records of icp_records_kernel for the reduce launch's
+// B x nbpp workgroup slots, added by the launch's pair reduction (p.fin.icp_rec)
+int launch_icp_records(IterParams& p, hipStream_t st) {
+  // S workgroups per slot, each with at least 8 pixels per thread
+  p.fin.icp_sub = std::max(1, std::min(kIcpSub, (int)((long)p.H * p.W / ((long)p.nbpp * kThreads * 8))));
+  hipLaunchKernelGGL(icp_records_kernel, dim3(p.B * p.nbpp * p.fin.icp_sub), dim3(kThreads), 0, st, p, p.icp_rec);
+  p.fin.icp_rec = p.icp_rec;
+  return hip_check("icp_records_kernel");
+}
+
 template <int CT, bool CS1, bool TRU, int MODE, bool C4 = false>
-int launch_reduce_k(IterParams p, hipStream_t st) {
+int launch_reduce_k(IterParams p, hipStream_t st, bool icp_pass = false) {
   const void* k = reinterpret_cast<const void*>(&ic_reduce_kernel<CT, CS1, TRU, MODE, C4>);
   const int cap = resident_blocks(k);
   if (cap <= 0) return fail(DPFT_E_HIP, "occupancy query failed");
@@ -3036,6 +3154,8 @@ int launch_reduce_k(IterParams p, hipStream_t st) {
   }
   p.round_wg = cap / 8;
   p.fin.nbpp = p.nbpp;
+  int rc;
+  if (icp_pass && (rc = launch_icp_records(p, st))) return rc;
   // the finalize runs in-kernel (last-workgroup handshake, fin_on)
   hipLaunchKernelGGL((ic_reduce_kernel<CT, CS1, TRU, MODE, C4>), dim3(p.B * p.nbpp), dim3(kThreads), 0, st, p);
   return DPFT_OK;
@@ -3058,13 +3178,15 @@ int launch_reduce_t(const IterParams& p, hipStream_t st) {
 }
 
 template <int CT, bool TRU, int MODE>
-int launch_split(IterParams p, hipStream_t st) {
+int launch_split(IterParams p, hipStream_t st, bool icp_pass = false) {
   const void* k = reinterpret_cast<const void*>(&ic_split_kernel<CT, TRU, MODE>);
   const int cap = resident_blocks(k);
   if (cap <= 0) return fail(DPFT_E_HIP, "occupancy query failed");
   const int units = p.tiles_x * p.H;
   p.nbpp = std::max(1, std::min(cap / p.B, units));
   p.fin.nbpp = p.nbpp;
+  int rc;
+  if (icp_pass && (rc = launch_icp_records(p, st))) return rc;
   // Many small workgroups finish together here: the last-block handshake would
   // serialise B * nbpp atomics on B counters, so the finalize is its own launch
   // (B workgroups, the kernel boundary orders the records).
@@ -3083,12 +3205,17 @@ int launch_reduce_c4(const IterParams& p, hipStream_t st) {
     if (sched == DPFT_SCHED_AUTO)  // coarse levels (few pixels per pair): the channel-split kernel
       sched = ((long)p.H * p.W <= kSplitMaxPixels && (long)p.B * p.H * p.W <= kSplitMaxLaunchPixels)
                   ? DPFT_SCHED_SPLIT : DPFT_SCHED_MARCH;
-    if (!(p.flags & DPFT_COMBINE_ICP) && !p.wgt) {  // combine_ICP / M-estimator weights: ic_reduce_kernel
+    // combine_ICP: the U_IC kernels plus the point-to-plane term's own pass (icp_records_kernel)
+    const bool icp = (p.flags & DPFT_COMBINE_ICP) != 0;
+    if (!p.wgt) {  // M-estimator weights: ic_reduce_kernel
       if (sched == DPFT_SCHED_SPLIT) {
         if (p.flags & DPFT_NO_UNCERTAINTY) return launch_split<CT, false, 2>(p, st);
-        return tru ? launch_split<CT, true, 0>(p, st) : launch_split<CT, false, 0>(p, st);
+        return tru ? launch_split<CT, true, 0>(p, st, icp) : launch_split<CT, false, 0>(p, st, icp);
       }
     }
+    if (icp)
+      return tru ? launch_reduce_k<CT, true, true, 0, true>(p, st, true)
+                 : launch_reduce_k<CT, true, false, 0, true>(p, st, true);
   }
   if (p.flags & DPFT_NO_UNCERTAINTY) return launch_reduce_k<CT, true, false, 2, true>(p, st);
   if (p.flags & DPFT_COMBINE_ICP)

@@ -52,17 +52,24 @@ def run_pass(counter, outdir, groups, icp=False):
 
 
 def parse(counter, outdir):
-    rows = []
+    rows, icp_rows = [], []
     for f in glob.glob(os.path.join(outdir, "**", "*counter_collection.csv"), recursive=True):
         for r in csv.DictReader(open(f)):
-            if "ic_reduce_kernel" in r["Kernel_Name"] and r["Counter_Name"] == counter:
+            if r["Counter_Name"] != counter:
+                continue
+            if "ic_reduce_kernel" in r["Kernel_Name"]:
                 rows.append((int(r["Dispatch_Id"]), float(r["Counter_Value"])))
+            elif "icp_records_kernel" in r["Kernel_Name"]:  # combine_ICP's own pass, one per reduce launch
+                icp_rows.append((int(r["Dispatch_Id"]), float(r["Counter_Value"])))
     # the last LEVEL0_LAUNCHES are kbench's level-0 launches (its first iteration + reps x 3);
     # before them, its --from-solve pyramid solve (marching launches per level depend on
     # the batch size: levels 1 and 0 at 8 pairs, every level at 128)
     vals = [v for _, v in sorted(rows)[-LEVEL0_LAUNCHES:]]
     if not vals:
         raise SystemExit(f"no ic_reduce_kernel rows for {counter}")
+    if icp_rows:  # a level-0 iteration is the ICP pass + the reduce launch: their bytes together
+        ivals = [v for _, v in sorted(icp_rows)[-LEVEL0_LAUNCHES:]]
+        vals = [a + b for a, b in zip(vals, ivals)]
     return sum(vals) / len(vals), len(vals)
 
 
@@ -82,8 +89,8 @@ def main():
         write, nw = run_pass("WRITE_SIZE", os.path.join(tmp, "write"), a.groups, a.icp)
     sys.path.insert(0, ROOT)
     from deep_prob_feature_track_amd import build as B
-    kernel = B.ICP_KERNEL if a.icp else B.L0_KERNEL
-    out = {"kernel": f"ic_reduce_kernel<32,Cs=1,tru,{'U_IC+ICP' if a.icp else 'U_IC'},c4> level 0, {a.groups} x 8 pairs per launch, 640x480 "
+    kernel = B.L0_KERNEL
+    out = {"kernel": f"ic_reduce_kernel<32,Cs=1,tru,U_IC,c4>{' + icp_records_kernel' if a.icp else ''} level 0, {a.groups} x 8 pairs per launch, 640x480 "
                      "(tools/kbench.py --mode level --from-solve)",
            "pairs_per_launch": 8 * a.groups, "group": 8,
            "src_sha256": src_sha(), "isa_sha256": isa_sha(kernel), "combine_icp": a.icp, "launches": {"fetch": nf, "write": nw},
