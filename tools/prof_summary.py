@@ -85,9 +85,9 @@ def main():
             continue
         layout = "nchw" if name.endswith("false>") else "c4"
         mode = "solo" if sid == solo_stream else "side streams"
-        if name.startswith(("ic_reduce", "ic_split", "finalize", "minmax", "icp_normals")):
-            groups[(mode, layout if not name.startswith(("finalize", "minmax", "icp_normals")) else "-", level,
-                    name)].append(dur)
+        if name.startswith(("ic_reduce", "ic_split", "finalize", "minmax", "icp_normals", "icp_records")):
+            groups[(mode, layout if not name.startswith(("finalize", "minmax", "icp_normals", "icp_records")) else "-",
+                    level, name)].append(dur)
         st["cur"].append((int(r["Start_Timestamp"]), dur, level, name,
                           int(r["Grid_Size_X"]) // max(int(r["Workgroup_Size_X"]), 1)))
     for st in state.values():
