@@ -63,7 +63,6 @@ LLVM_BIN = "/opt/rocm/lib/llvm/bin"
 ISA_OUT = os.path.join(HERE, "libdpft_ic.isa.json")
 # the level-0/1 marching kernel of the bench (C = 32, one sigma plane, remove_tru_sigma, U_IC, channel quads)
 L0_KERNEL = "_ZN12_GLOBAL__N_116ic_reduce_kernelILi32ELb1ELb1ELi0ELb1EEEvNS_10IterParamsE"
-ICP_KERNEL = L0_KERNEL.replace("ELi0ELb1E", "ELi1ELb1E")  # the same with the combine_ICP term (bench.py --icp)
 
 
 def isa_hashes(so_path=OUT):

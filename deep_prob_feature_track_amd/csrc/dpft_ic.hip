@@ -3218,8 +3218,10 @@ int launch_reduce_c4(const IterParams& p, hipStream_t st) {
                  : launch_reduce_k<CT, true, false, 0, true>(p, st, true);
   }
   if (p.flags & DPFT_NO_UNCERTAINTY) return launch_reduce_k<CT, true, false, 2, true>(p, st);
-  if (p.flags & DPFT_COMBINE_ICP)
-    return tru ? launch_reduce_k<CT, true, true, 1, true>(p, st) : launch_reduce_k<CT, true, false, 1, true>(p, st);
+  if constexpr (!(CT > 0 && CT % 16 == 0)) {  // (C % 16 == 0: the ICP pass above, no fused instance)
+    if (p.flags & DPFT_COMBINE_ICP)
+      return tru ? launch_reduce_k<CT, true, true, 1, true>(p, st) : launch_reduce_k<CT, true, false, 1, true>(p, st);
+  }
   return tru ? launch_reduce_k<CT, true, true, 0, true>(p, st) : launch_reduce_k<CT, true, false, 0, true>(p, st);
 }
 
