@@ -88,7 +88,7 @@ constexpr int kGridWaste = DPFT_GRID_WASTE;  // marching band grid: idle waves a
 // ---- reduce-record layout (floats) ------------------------------------------
 constexpr int kRec = 48;
 constexpr int kIcpRec = 32;  // icp_records_kernel record: JtJ (21) + JtR (6) + 0 (the invalid count's slot), padded
-constexpr int kIcpSub = 4;   // icp_records_kernel: at most this many workgroups (records) per reduce workgroup slot
+constexpr int kIcpSub = DPFT_ICP_SUB;  // icp_records_kernel: at most this many workgroups (records) per reduce slot
 constexpr int kIcpTab = 2048;  // icp_records_kernel: normalised-coordinate table in LDS when W + H fits
 constexpr int R_NINV = 27;    // invalid pixels (occlusion | masks | sigma0-trunc)
 constexpr int R_MN_ALL = 28;  // min of sigma_r over every channel

@@ -32,6 +32,10 @@
 #ifndef DPFT_RING_Q
 #define DPFT_RING_Q 4
 #endif
+// combine_ICP pass (icp_records_kernel): at most this many workgroups per reduce workgroup slot
+#ifndef DPFT_ICP_SUB
+#define DPFT_ICP_SUB 4
+#endif
 // sigma0 / depth extrema pass: workgroups and 16-byte loads in flight per thread
 #ifndef DPFT_MM_GRID
 #define DPFT_MM_GRID 128

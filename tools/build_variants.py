@@ -7,7 +7,7 @@ python tools/build_variants.py name=@path/to/experiment.hip[:-DFLAG=V,...] ...  
 
 The shipped source has no alternative code paths; a variant only moves the numeric operating
 point of csrc/dpft_tuning.h (DPFT_SPLIT_MAX_PIXELS, DPFT_SPLIT_MAX_LAUNCH_PIXELS,
-DPFT_MARCH_SKEW, DPFT_GRID_WASTE, DPFT_MARCH_MIN_ROWS, DPFT_RING_Q, DPFT_MM_GRID, DPFT_MM_LOADS, DPFT_PROBE_GRID, DPFT_PROBE_DEPTH).
+DPFT_MARCH_SKEW, DPFT_GRID_WASTE, DPFT_MARCH_MIN_ROWS, DPFT_RING_Q, DPFT_ICP_SUB, DPFT_MM_GRID, DPFT_MM_LOADS, DPFT_PROBE_GRID, DPFT_PROBE_DEPTH).
 """
 import os
 import subprocess
