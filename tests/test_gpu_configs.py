@@ -83,6 +83,11 @@ def _assert_within_reference_envelope(R, t, z, what=""):
         over = np.flatnonzero(dev > SE3_TOL)
     print(f"{what}: {dev.size - over.size} of {dev.size} pairs within 1e-4 of both reference runs; max vs fp32 "
           f"{dev.max():.2e}" + (f", vs fp64 {dev64.max():.2e}" if "f64_R" in z else ""))
+    print(f"  vs the fp32 run alone: {int((dev <= SE3_TOL).sum())} of {dev.size} within 1e-4, "
+          f"{int((dev <= floor).sum())} within the noise floor"
+          + (f"; vs the fp64 run: {int((dev64 <= SE3_TOL).sum())} within 1e-4, "
+             f"{int((dev64 <= d3264 + SE3_TOL).sum())} within the reference's own fp32-fp64 distance + 1e-4"
+             if "f64_R" in z else ""))
     if over.size:
         print("  beyond 1e-4 (pair: vs fp32 / vs fp64 / reference noise floor / reference fp32-fp64):",
               {int(b): (f"{dev[b]:.2e}", f"{dev64[b]:.2e}" if "f64_R" in z else "-", f"{floor[b]:.2e}",
