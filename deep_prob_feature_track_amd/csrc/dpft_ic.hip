@@ -247,13 +247,33 @@ struct Taps {
 // geometry.py:359-364 normalises u,v to [-1,1]; grid_sample(align_corners=True,
 // padding_mode='border') maps back with (g + 1) * (size - 1) / 2, clamps to
 // [0, size-1], and weighs the four neighbours by products of the distances.
+// a / b for a divisor b that is constant across the launch, given rb = RN(1 / b): one product
+// and one FMA correction (Markstein's theorem: with rb the correctly rounded reciprocal and the
+// product within an ulp of the quotient, q + (a - b q) rb rounds to the correctly rounded
+// quotient).  make_taps_xy uses it on |a| <= 2^30 (larger and NaN coordinates are clamped
+// there first: the taps clamp to the image border either way), where only quotients of
+// magnitude >= 2^-25 can move a tap; in that domain it equals the IEEE division for every
+// float a: tools/div_check.c checks all 2^32 floats for b = 319.5, 159.5, 79.5, 39.5, 239.5,
+// 119.5, 59.5, 29.5 (the bench's levels) and a stride through all floats for every
+// b = (n - 1) / 2, n = 2 .. 8192.
+__device__ __forceinline__ float div_const(float a, float b, float rb) {
+  const float q = a * rb;
+  return __builtin_fmaf(__builtin_fmaf(-q, b, a), rb, q);
+}
 __device__ __forceinline__ Taps make_taps_xy(float u, float v, int H, int W, int& tx0, int& tx1, int& ty0,
-                                             int& ty1) {
+                                             int& ty1, const float* rs = nullptr) {
 #pragma clang fp contract(off)
   const float sx = (float)(W - 1) * 0.5f;
   const float sy = (float)(H - 1) * 0.5f;
-  float ix = ((u / sx) - 1.0f + 1.0f) * sx;
-  float iy = ((v / sy) - 1.0f + 1.0f) * sy;
+  float ix, iy;
+  if (rs) {  // rs = RN(1 / sx), RN(1 / sy) (the combine_ICP pass, computed once per workgroup)
+    const float uc = fminf(fmaxf(u, -0x1p30f), 0x1p30f), vc = fminf(fmaxf(v, -0x1p30f), 0x1p30f);
+    ix = (div_const(uc, sx, rs[0]) - 1.0f + 1.0f) * sx;
+    iy = (div_const(vc, sy, rs[1]) - 1.0f + 1.0f) * sy;
+  } else {
+    ix = ((u / sx) - 1.0f + 1.0f) * sx;
+    iy = ((v / sy) - 1.0f + 1.0f) * sy;
+  }
   ix = fminf(fmaxf(ix, 0.0f), (float)(W - 1));
   iy = fminf(fmaxf(iy, 0.0f), (float)(H - 1));
   const float fx0 = floorf(ix), fy0 = floorf(iy);
@@ -614,7 +634,7 @@ struct IcpTaps {
 
 __device__ __forceinline__ IcpGeo icp_geo(float xr, float yr, float d0, const float* __restrict__ Rm,
                                           const float* __restrict__ tv, float fx, float fy, float cx, float cy, int H,
-                                          int W) {
+                                          int W, const float* rs = nullptr) {
 #pragma clang fp contract(off)
   IcpGeo g;
   // vertex0 = [px, py, 1] * depth0; P = R V0 + t (CPU bmm order, then + t)
@@ -629,7 +649,7 @@ __device__ __forceinline__ IcpGeo icp_geo(float xr, float yr, float d0, const fl
   g.inview = (u > 0.0f) && (u < (float)(W - 1)) && (v > 0.0f) && (v < (float)(H - 1));
   // (the taps are clamped into the image whatever u, v are -- NaN included -- so the loads
   // below stay in bounds on every lane)
-  g.tp = make_taps_xy(u, v, H, W, g.x0, g.x1, g.y0, g.y1);
+  g.tp = make_taps_xy(u, v, H, W, g.x0, g.x1, g.y0, g.y1, rs);
   return g;
 }
 
@@ -778,6 +798,8 @@ __global__ __launch_bounds__(kThreads) void icp_records_kernel(IterParams p, flo
     for (int j = tid; j < W + H; j += kThreads) nxy[j] = j < W ? norm_coord(j, cx, fx) : norm_coord(j - W, cy, fy);
     __syncthreads();
   }
+  // the tap computation's divisors' reciprocals (make_taps_xy: exact division by a constant)
+  const float rsxy[2] = {1.0f / ((float)(W - 1) * 0.5f), 1.0f / ((float)(H - 1) * 0.5f)};
   auto ncx = [&](int x) { return tab ? nxy[x] : norm_coord(x, cx, fx); };
   auto ncy = [&](int y) { return tab ? nxy[W + y] : norm_coord(y, cy, fy); };
   const float* d0b = p.depth0 + (size_t)b * HW;
@@ -792,7 +814,7 @@ __global__ __launch_bounds__(kThreads) void icp_records_kernel(IterParams p, flo
   for (; pix < end; pix += kThreads) {
     const bool m0 = m0b ? (m0b[pix] != 0) : true;
     const float d0 = d0b[pix];
-    const IcpGeo g = icp_geo(ncx(x), ncy(y), d0, Rm, tv, fx, fy, cx, cy, H, W);
+    const IcpGeo g = icp_geo(ncx(x), ncy(y), d0, Rm, tv, fx, fy, cx, cy, H, W, rsxy);
     const IcpTapXY n{ncx(g.x0), ncx(g.x1), ncy(g.y0), ncy(g.y1)};
     const IcpTerm ic = icp_term(g, icp_load(g, nd1), n, d0, Rm, !m0, m1b, p.icp_w);
     int kq = 0;
