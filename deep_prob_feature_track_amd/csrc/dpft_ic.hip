@@ -260,13 +260,15 @@ __device__ __forceinline__ float div_const(float a, float b, float rb) {
   const float q = a * rb;
   return __builtin_fmaf(__builtin_fmaf(-q, b, a), rb, q);
 }
+// RC: rs = RN(1 / sx), RN(1 / sy) given (the combine_ICP pass computes them once per workgroup)
+template <bool RC = false>
 __device__ __forceinline__ Taps make_taps_xy(float u, float v, int H, int W, int& tx0, int& tx1, int& ty0,
                                              int& ty1, const float* rs = nullptr) {
 #pragma clang fp contract(off)
   const float sx = (float)(W - 1) * 0.5f;
   const float sy = (float)(H - 1) * 0.5f;
   float ix, iy;
-  if (rs) {  // rs = RN(1 / sx), RN(1 / sy) (the combine_ICP pass, computed once per workgroup)
+  if constexpr (RC) {
     const float uc = fminf(fmaxf(u, -0x1p30f), 0x1p30f), vc = fminf(fmaxf(v, -0x1p30f), 0x1p30f);
     ix = (div_const(uc, sx, rs[0]) - 1.0f + 1.0f) * sx;
     iy = (div_const(vc, sy, rs[1]) - 1.0f + 1.0f) * sy;
@@ -649,7 +651,8 @@ __device__ __forceinline__ IcpGeo icp_geo(float xr, float yr, float d0, const fl
   g.inview = (u > 0.0f) && (u < (float)(W - 1)) && (v > 0.0f) && (v < (float)(H - 1));
   // (the taps are clamped into the image whatever u, v are -- NaN included -- so the loads
   // below stay in bounds on every lane)
-  g.tp = make_taps_xy(u, v, H, W, g.x0, g.x1, g.y0, g.y1, rs);
+  g.tp = rs ? make_taps_xy<true>(u, v, H, W, g.x0, g.x1, g.y0, g.y1, rs)
+            : make_taps_xy<false>(u, v, H, W, g.x0, g.x1, g.y0, g.y1);
   return g;
 }
 
