@@ -44,6 +44,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <type_traits>
 #include <cmath>
 #include <cstdarg>
 #include <cstdint>
@@ -803,8 +804,6 @@ __global__ __launch_bounds__(kThreads) void icp_records_kernel(IterParams p, flo
   }
   // the tap computation's divisors' reciprocals (make_taps_xy: exact division by a constant)
   const float rsxy[2] = {1.0f / ((float)(W - 1) * 0.5f), 1.0f / ((float)(H - 1) * 0.5f)};
-  auto ncx = [&](int x) { return tab ? nxy[x] : norm_coord(x, cx, fx); };
-  auto ncy = [&](int y) { return tab ? nxy[W + y] : norm_coord(y, cy, fy); };
   const float* d0b = p.depth0 + (size_t)b * HW;
   const uint8_t* m0b = p.mask0 ? p.mask0 + (size_t)b * HW : nullptr;
   const uint8_t* m1b = p.mask1 ? p.mask1 + (size_t)b * HW : nullptr;
@@ -813,27 +812,37 @@ __global__ __launch_bounds__(kThreads) void icp_records_kernel(IterParams p, flo
   float acc[27];
 #pragma unroll
   for (int i = 0; i < 27; ++i) acc[i] = 0.f;
-  int pix = beg + tid, y = pix / W, x = pix - y * W;  // then advanced by kThreads without a division
-  for (; pix < end; pix += kThreads) {
-    const bool m0 = m0b ? (m0b[pix] != 0) : true;
-    const float d0 = d0b[pix];
-    const IcpGeo g = icp_geo(ncx(x), ncy(y), d0, Rm, tv, fx, fy, cx, cy, H, W, rsxy);
-    const IcpTapXY n{ncx(g.x0), ncx(g.x1), ncy(g.y0), ncy(g.y1)};
-    const IcpTerm ic = icp_term(g, icp_load(g, nd1), n, d0, Rm, !m0, m1b, p.icp_w);
-    int kq = 0;
+  // the pixel loop, instantiated with and without the table (no per-use branches)
+  auto pixels = [&](auto table) {
+    constexpr bool TAB = decltype(table)::value;
+    auto ncx = [&](int x) { return TAB ? nxy[x] : norm_coord(x, cx, fx); };
+    auto ncy = [&](int y) { return TAB ? nxy[W + y] : norm_coord(y, cy, fy); };
+    int pix = beg + tid, y = pix / W, x = pix - y * W;  // then advanced by kThreads without a division
+    for (; pix < end; pix += kThreads) {
+      const bool m0 = m0b ? (m0b[pix] != 0) : true;
+      const float d0 = d0b[pix];
+      const IcpGeo g = icp_geo(ncx(x), ncy(y), d0, Rm, tv, fx, fy, cx, cy, H, W, rsxy);
+      const IcpTapXY n{ncx(g.x0), ncx(g.x1), ncy(g.y0), ncy(g.y1)};
+      const IcpTerm ic = icp_term(g, icp_load(g, nd1), n, d0, Rm, !m0, m1b, p.icp_w);
+      int kq = 0;
 #pragma unroll
-    for (int i = 0; i < 6; ++i) {
+      for (int i = 0; i < 6; ++i) {
 #pragma unroll
-      for (int j = i; j < 6; ++j) acc[kq++] += ic.J[i] * ic.J[j];
+        for (int j = i; j < 6; ++j) acc[kq++] += ic.J[i] * ic.J[j];
+      }
+#pragma unroll
+      for (int i = 0; i < 6; ++i) acc[21 + i] += ic.J[i] * ic.r;
+      x += kThreads;
+      while (x >= W) {
+        x -= W;
+        ++y;
+      }
     }
-#pragma unroll
-    for (int i = 0; i < 6; ++i) acc[21 + i] += ic.J[i] * ic.r;
-    x += kThreads;
-    while (x >= W) {
-      x -= W;
-      ++y;
-    }
-  }
+  };
+  if (tab)
+    pixels(std::true_type{});
+  else
+    pixels(std::false_type{});
   // fixed-order reduction: wave butterflies, then the four waves in order
 #pragma unroll
   for (int i = 0; i < 27; ++i) {
