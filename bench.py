@@ -48,14 +48,14 @@ def parse():
                    help="> 0: weak scaling instead, this many pairs per GPU per step")
     p.add_argument("--batch", type=int, default=8,
                    help="pairs per independent batch (one reference call: its own batch-global extrema)")
-    p.add_argument("--inflight", type=int, default=4,
-                   help="consecutive steps of the stream in flight per GPU (one stream, graph, workspace each)")
+    p.add_argument("--inflight", type=int, default=2,
+                   help="calls of the stream in flight per GPU (one stream, graph, workspace each)")
     p.add_argument("--stream-group", type=int, default=0,
                    help="global batches of the stream per grouped call on each rank (0: enough for "
                         "--min-launch-pairs pairs per call)")
-    p.add_argument("--min-launch-pairs", type=int, default=64,
-                   help="stream grouping target: pairs per call and rank (the N = 1 launch holds the whole "
-                        "64-pair global batch)")
+    p.add_argument("--min-launch-pairs", type=int, default=128,
+                   help="stream grouping target: pairs per call and rank (at N = 1 a call holds two 64-pair "
+                        "global batches; measured +1.5 %% against one batch per call with 4 in flight, DESIGN.md 4.8)")
     p.add_argument("--icp", action="store_true", help="cfg5: with the combine_ICP term (weight 0.01)")
     p.add_argument("--setup-warm-ms", type=float, default=200.0,
                    help="setup: replay solves for this long before the --warmup steps (the GPU clock ramps over "

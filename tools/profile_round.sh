@@ -17,7 +17,7 @@ bench_extra=""
 [ -n "$icp" ] && bench_extra="--icp --no-cpu-baseline --no-compare"
 ( cd /tmp && timeout -k 10 240 rocprofv3 --kernel-trace --stats --output-format csv -d "$root/gpurun_out/${tag}_prof" \
     -o bench -- python3 "$root/bench.py" --steps 100 --warmup 10 $bench_extra ) > "gpurun_out/${tag}_prof.log" 2>&1
-timeout -k 10 240 python tools/pmc_l0.py --groups 8 $icp --out "gpurun_out/${tag}_l0_traffic.json" > "gpurun_out/${tag}_traffic.log" 2>&1
+timeout -k 10 240 python tools/pmc_l0.py --groups 16 $icp --out "gpurun_out/${tag}_l0_traffic.json" > "gpurun_out/${tag}_traffic.log" 2>&1
 PMC_PASSES="$(cat tools/pmc_l0_passes.txt)" timeout -k 10 600 tools/pmc_passes.sh "gpurun_out/${tag}_pmc" -- \
-    python3 "$root/tools/kbench.py" --c4 --from-solve --mode level --reps 10 --warm-ms 0 --groups 8 $icp
+    python3 "$root/tools/kbench.py" --c4 --from-solve --mode level --reps 10 --warm-ms 0 --groups 16 $icp
 echo "profile set $tag done"
