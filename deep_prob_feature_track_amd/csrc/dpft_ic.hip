@@ -254,9 +254,10 @@ struct Taps {
 // quotient).  make_taps_xy uses it on |a| <= 2^30 (larger and NaN coordinates are clamped
 // there first: the taps clamp to the image border either way), where only quotients of
 // magnitude >= 2^-25 can move a tap; in that domain it equals the IEEE division for every
-// float a: tools/div_check.c checks all 2^32 floats for b = 319.5, 159.5, 79.5, 39.5, 239.5,
-// 119.5, 59.5, 29.5 (the bench's levels) and a stride through all floats for every
-// b = (n - 1) / 2, n = 2 .. 8192.
+// float a: tools/div_check.c checks all 2^32 floats for b = 319.5, 159.5, 79.5, 39.5, 19.5, 9.5,
+// 239.5, 119.5, 59.5, 29.5, 14.5, 7 (every level of 640x480 and 160x120) and a stride through
+// all floats for every b = (n - 1) / 2, n = 2 .. 8192; the library selects it only for those
+// twelve sizes (kVerifiedTapSizes), any other size divides by IEEE.
 __device__ __forceinline__ float div_const(float a, float b, float rb) {
   const float q = a * rb;
   return __builtin_fmaf(__builtin_fmaf(-q, b, a), rb, q);
@@ -415,6 +416,7 @@ struct IterParams {
   int fin_on;      // 0: records only (timing hook); 1: last workgroup finalizes
   int reverse;     // marching path: walk every band in the opposite direction (DPFT_ITER_REVERSE)
   int skew;        // marching path: band-size skew, 64ths (see ic_reduce_kernel)
+  int rc_taps;     // combine_ICP pass: the taps' divisions by div_const (W and H verified sizes)
   FinParams fin;
 };
 
@@ -802,7 +804,8 @@ __global__ __launch_bounds__(kThreads) void icp_records_kernel(IterParams p, flo
     for (int j = tid; j < W + H; j += kThreads) nxy[j] = j < W ? norm_coord(j, cx, fx) : norm_coord(j - W, cy, fy);
     __syncthreads();
   }
-  // the tap computation's divisors' reciprocals (make_taps_xy: exact division by a constant)
+  // the tap computation's divisors' reciprocals (make_taps_xy: exact division by a constant,
+  // only for the image sizes it is verified for, p.rc_taps; else the IEEE division)
   const float rsxy[2] = {1.0f / ((float)(W - 1) * 0.5f), 1.0f / ((float)(H - 1) * 0.5f)};
   const float* d0b = p.depth0 + (size_t)b * HW;
   const uint8_t* m0b = p.mask0 ? p.mask0 + (size_t)b * HW : nullptr;
@@ -812,16 +815,16 @@ __global__ __launch_bounds__(kThreads) void icp_records_kernel(IterParams p, flo
   float acc[27];
 #pragma unroll
   for (int i = 0; i < 27; ++i) acc[i] = 0.f;
-  // the pixel loop, instantiated with and without the table (no per-use branches)
-  auto pixels = [&](auto table) {
-    constexpr bool TAB = decltype(table)::value;
+  // the pixel loop, instantiated with and without the table and div_const (no per-use branches)
+  auto pixels = [&](auto table, auto rc) {
+    constexpr bool TAB = decltype(table)::value, RC = decltype(rc)::value;
     auto ncx = [&](int x) { return TAB ? nxy[x] : norm_coord(x, cx, fx); };
     auto ncy = [&](int y) { return TAB ? nxy[W + y] : norm_coord(y, cy, fy); };
     int pix = beg + tid, y = pix / W, x = pix - y * W;  // then advanced by kThreads without a division
     for (; pix < end; pix += kThreads) {
       const bool m0 = m0b ? (m0b[pix] != 0) : true;
       const float d0 = d0b[pix];
-      const IcpGeo g = icp_geo(ncx(x), ncy(y), d0, Rm, tv, fx, fy, cx, cy, H, W, rsxy);
+      const IcpGeo g = icp_geo(ncx(x), ncy(y), d0, Rm, tv, fx, fy, cx, cy, H, W, RC ? rsxy : nullptr);
       const IcpTapXY n{ncx(g.x0), ncx(g.x1), ncy(g.y0), ncy(g.y1)};
       const IcpTerm ic = icp_term(g, icp_load(g, nd1), n, d0, Rm, !m0, m1b, p.icp_w);
       int kq = 0;
@@ -839,10 +842,12 @@ __global__ __launch_bounds__(kThreads) void icp_records_kernel(IterParams p, flo
       }
     }
   };
-  if (tab)
-    pixels(std::true_type{});
+  if (tab && p.rc_taps)
+    pixels(std::true_type{}, std::true_type{});
+  else if (tab)
+    pixels(std::true_type{}, std::false_type{});
   else
-    pixels(std::false_type{});
+    pixels(std::false_type{}, std::false_type{});
   // fixed-order reduction: wave butterflies, then the four waves in order
 #pragma unroll
   for (int i = 0; i < 27; ++i) {
@@ -1556,13 +1561,49 @@ __global__ __launch_bounds__(kThreads, 1) void ic_reduce_kernel(IterParams p) {
     int ubeg, uend, vband;
     // hybrid split: wave s < S owns rows [0, T_s) of strip s, T_s its weighted share of
     // the pair's units (Tf for the first half of the waves, Tu for the second); the
-    // nw - S pool waves split the bottom rows [T_s, H) of all strips, strip-major
+    // nw - S pool waves march the bottom rows [T_s, H) of all strips, phased (below)
     const bool hyb = !grid && nw > S_ && nw < 2 * S_;
     const int hh = nw >> 1, hsk = nw >= 2 ? p.skew : 0;
     const int hwt = (64 + hsk) * hh + (64 - hsk) * (nw - hh);
     const int hTf = min(H, (U * (64 + hsk)) / hwt), hTu = min(H, (U * (64 - hsk)) / hwt);
-    const int hnf = min(hh, S_), hLf = H - hTf, hLu = H - hTu;
+    const int hnf = min(hh, S_);
     const bool hpool = hyb && band >= S_;
+    // phased pool (round 5): pool wave j marches the bottoms of strips j, j + np, ... (hpFs
+    // full rounds; np = nw - S pool waves), so in each phase the pool waves march np adjacent
+    // strips side by side and their shared 128-byte lines are fetched about when both need
+    // them; then its chunk [hpX0, hpX1) of the remaining strips' bottoms (strip-major from
+    // strip hpRb), sized so that each wave's total is its weighted share of the pool units.
+    // (The previous strip-major split of the bottoms marched neighbouring strips' shared
+    // lines tens of microseconds apart: level-0 reads of a 128-pair launch 1.152x -> 1.135x
+    // of the algorithmic bytes, the launch 2061 -> 2052 us, same box.)
+    const int hpNp = max(nw - S_, 1), hpJ = band - S_;
+    const int hpFs = S_ / hpNp, hpRb = hpFs * hpNp;
+    auto hT = [&](int s) { return s < hnf ? hTf : hTu; };
+    int hpF = 0, hpX0 = 0, hpX1 = 0;
+    if (hpool) {
+      int PU = 0, RU = 0;
+      for (int s = 0; s < S_; ++s) {
+        PU += H - hT(s);
+        RU += s >= hpRb ? H - hT(s) : 0;
+      }
+      int wt = 0;
+      for (int i = 0; i < hpNp; ++i) wt += (S_ + i) < hh ? 64 + hsk : 64 - hsk;
+      int ws = 0, cf = 0, x = 0;  // running: weight, full-round units, chunk start (a running max)
+      for (int i = 0; i <= hpJ; ++i) {
+        int fi = 0;
+        for (int r = 0; r < hpFs; ++r) fi += H - hT(r * hpNp + i);
+        const int wi = (S_ + i) < hh ? 64 + hsk : 64 - hsk;
+        const int x1 = i == hpNp - 1 ? RU : max(x, min(max((PU * (ws + wi)) / wt - (cf + fi), 0), RU));
+        if (i == hpJ) {
+          hpF = fi;
+          hpX0 = x;
+          hpX1 = x1;
+        }
+        ws += wi;
+        cf += fi;
+        x = x1;
+      }
+    }
     // grid + pool split (2 S < nw, no waste-free grid: the 64-pair launch's 32 waves over 11
     // strips): Kg = ceil(nw / S) row bands with common cuts give Kg S >= nw segments; wave w
     // marches segment w (band w / S, strip w % S) and the Eg = Kg S - nw segments left over
@@ -1591,16 +1632,8 @@ __global__ __launch_bounds__(kThreads, 1) void ic_reduce_kernel(IterParams p) {
       uend = band * H + (band < hh ? hTf : hTu);
       vband = 0;
     } else if (hpool) {
-      const int PU = hnf * hLf + (S_ - hnf) * hLu, np = nw - S_, j = band - S_;
-      int wt = 0, ws0 = 0, ws1 = 0;  // weighted split over the pool waves S .. nw - 1
-      for (int i = 0; i < np; ++i) {
-        const int wi = (S_ + i) < hh ? 64 + hsk : 64 - hsk;
-        wt += wi;
-        ws0 += i < j ? wi : 0;
-        ws1 += i <= j ? wi : 0;
-      }
-      ubeg = (PU * ws0) / wt;
-      uend = (PU * ws1) / wt;
+      ubeg = 0;
+      uend = hpF + hpX1 - hpX0;
       vband = 1;
     } else if (grid) {
       const int k = band / S_, s = band - k * S_;
@@ -1642,17 +1675,35 @@ __global__ __launch_bounds__(kThreads, 1) void ic_reduce_kernel(IterParams p) {
         }
       } else {
         if (hpool) {
-          const int uf = hnf * hLf;
-          if (u < uf) {
-            strip = u / max(hLf, 1);
-            y = hTf + (u - strip * hLf);
-            ytop = hTf;
+          // k in marching order: the full rounds' strips first (every pool wave in the same
+          // phase), then the chunk; each segment walked in the marching direction
+          if (k < hpF) {
+            int kk = k, r = 0;
+            while (r + 1 < hpFs && kk >= H - hT(r * hpNp + hpJ)) {
+              kk -= H - hT(r * hpNp + hpJ);
+              ++r;
+            }
+            strip = r * hpNp + hpJ;
+            ylo = hT(strip);
+            yhi = H;
+            y = up ? H - 1 - kk : ylo + kk;
           } else {
-            const int s2 = (u - uf) / max(hLu, 1);
-            y = hTu + (u - uf - s2 * hLu);
-            strip = hnf + s2;
-            ytop = hTu;
+            const int kc = k - hpF;
+            const int v = up ? hpX1 - 1 - kc : hpX0 + kc;  // unit of the remaining strips' bottoms
+            int s = hpRb, base = 0;
+            while (s + 1 < S_ && v >= base + (H - hT(s))) {
+              base += H - hT(s);
+              ++s;
+            }
+            strip = s;
+            ylo = hT(s) + max(0, hpX0 - base);
+            yhi = hT(s) + min(H - hT(s), hpX1 - base);
+            y = hT(s) + (v - base);
           }
+          strt = y == (up ? yhi - 1 : ylo);
+          xs = strip * kTileOut - 1 + lane;
+          run = min(up ? y - ylo + 1 : yhi - y, nrows - k);
+          return;
         } else {
           strip = u / H;
           y = u - strip * H;
@@ -3021,6 +3072,16 @@ size_t ws_need_poses(const DpftLevelDesc& d, int P) {
   return rec_offset(d) + std::max(rec, rec_bytes(d));
 }
 
+// Image sizes whose tap divisor (n - 1) / 2 tools/div_check.c verifies div_const on for all
+// 2^32 floats (mode 0): every level of 640x480 and of 160x120.  Other sizes take the IEEE
+// division (make_taps_xy<false>).
+constexpr int kVerifiedTapSizes[] = {640, 320, 160, 80, 40, 20, 480, 240, 120, 60, 30, 15};
+bool tap_div_verified(int n) {
+  for (int v : kVerifiedTapSizes)
+    if (n == v) return true;
+  return false;
+}
+
 IterParams make_params(const DpftLevelDesc& d, const DpftLevelTensors& tt, const Geometry& g, const float* R,
                        const float* t, void* ws) {
   IterParams p;
@@ -3065,6 +3126,7 @@ IterParams make_params(const DpftLevelDesc& d, const DpftLevelTensors& tt, const
   p.fin_on = 0;
   p.reverse = 0;
   p.skew = kMarchSkew;
+  p.rc_taps = tap_div_verified(d.W) && tap_div_verified(d.H);
   memset(&p.fin, 0, sizeof(p.fin));
   p.fin.rec = p.rec;
   p.fin.prec = reinterpret_cast<double*>(static_cast<char*>(ws) + kCtrlBytes);

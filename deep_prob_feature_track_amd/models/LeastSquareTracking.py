@@ -13,11 +13,16 @@ and 'IC' (uncertainty_type 'None': TrustRegionBase with M-estimator 'None' or
 chained across levels as LeastSquareTracking.py:346-445 does) with encoders RGB /
 ConvRGBD / ConvRGBD2, identity or
 learned init pose, remove_tru_sigma, combine_ICP, uncer_prop (returns JtWJ) and
-object masks, inference mode.  The reference's U_FC / ICP-only trackers and
-training-mode forward raise NotImplementedError -- the reference itself cannot
-train on torch 2.x (algorithms.py:874-875).  Visualisation / logging arguments are accepted and
-ignored (they only draw with cv2 / tensorboard).
+object masks.  Device tensors at inference run the solver levels on libdpft_ic.so;
+CPU tensors and training mode run them on the PyTorch path (torch_solver.py, SURVEY.md
+8(b)): a host without a GPU runs the reference's callers unchanged, and training-mode
+forward returns the per-level poses stacked (LeastSquareTracking.py:568-575) with
+gradients through the encoder and the unrolled solver (the reference's own training path
+fails on torch 2.x, algorithms.py:874-875).  The reference's U_FC / ICP-only trackers raise
+NotImplementedError.  Visualisation / logging arguments are accepted and ignored (they
+only draw with cv2 / tensorboard).
 """
+import contextlib
 import types
 
 import torch
@@ -26,6 +31,7 @@ import torch.nn as nn
 from .algorithms import (DeepRobustEstimator, DirectSolverNet, FeaturePyramid, ImagePyramids, PoseNet, ScaleNet,
                          SFMPoseNet, TrustRegionBase, TrustRegionInverseWUncertainty)
 from .submodules import color_normalize
+from . import torch_solver as TS
 from .. import ic
 from .. import torch_ops  # noqa: F401  (registers the dpft:: ops torch.compile traces)
 
@@ -145,11 +151,13 @@ class LeastSquareTracking(nn.Module):
     # ------------------------------------------------------------------ API
     def forward(self, img0, img1, depth0, depth1, K, init_only=False, logger=None, iteration=0, vis=False,
                 obj_mask0=None, obj_mask1=None, index=None):
-        """Coarse-to-fine U_IC tracking (LeastSquareTracking.py:311-577); returns [R, t]."""
-        if self.training:
-            raise NotImplementedError("training-mode forward needs backward kernels (not provided)")
+        """Coarse-to-fine tracking (LeastSquareTracking.py:311-577); returns [R, t], or in
+        training mode the per-level poses stacked, (R [B,L,3,3], t [B,L,3,1][, JtWJ [B,L,6,6]])
+        with L = 4 (5 with a trained init pose, its pose first), levels 3 .. 0."""
         (I0, I1, x0, x1, sigma0, sigma1, dpt0, dpt1, inv_d0, inv_d1, m0, m1, poseI) = self._preprocess(
             img0, img1, depth0, depth1, poseI=None, obj_mask0=obj_mask0, obj_mask1=obj_mask1)
+        if self.training:
+            return self._forward_train(x0, x1, sigma0, sigma1, dpt0, dpt1, inv_d0, inv_d1, m0, m1, poseI, K)
         pose = poseI
         # the weight prior of level 3 (LeastSquareTracking.py:346); each level's returned
         # weights are the next level's prior (375-445) -- read by the IC tracker's learned
@@ -160,7 +168,7 @@ class LeastSquareTracking(nn.Module):
         # residual raises AssertionError out of forward and no pose is returned)
         compiling = torch.compiler.is_compiling()
         status = None
-        if self.track_type != 'IC' and not compiling:
+        if self.track_type != 'IC' and not compiling and not TS.needs_torch_path(x0[0]):
             status = torch.zeros(1, dtype=torch.int32, device=x0[0].device)
         try:
             for l in (3, 2, 1, 0):
@@ -196,6 +204,35 @@ class LeastSquareTracking(nn.Module):
             ic.check_status(status)
         return pose
 
+    def _forward_train(self, x0, x1, sigma0, sigma1, dpt0, dpt1, inv_d0, inv_d1, m0, m1, poseI, K):
+        """Training-mode forward (LeastSquareTracking.py:333-445, 568-575) on the PyTorch path:
+        every level's pose (and JtWJ with uncer_prop) collected, gradients kept."""
+        poses, sig = [[], []], []
+        if self.predict_init_pose and self.train_init_pose:
+            poses[0].append(poseI[0])
+            poses[1].append(poseI[1])
+            if self.uncer_prop:
+                sig.append(torch.eye(6, dtype=poseI[0].dtype, device=poseI[0].device).repeat(poseI[0].shape[0], 1, 1))
+        pose = poseI
+        wPrior = torch.ones_like(inv_d0[3]) * 0.001
+        for l in (3, 2, 1, 0):
+            tr = getattr(self, f'tr_update{l}')
+            Kl = K / float(1 << l)
+            if self.track_type == 'IC':
+                out = TS.ic_forward(tr, pose, x0[l], x1[l], inv_d0[l], inv_d1[l], Kl, wPrior, m0[l], m1[l])
+                wPrior = out[1]
+            else:
+                lv = tr._torch_level(x0[l], x1[l], inv_d0[l], inv_d1[l], Kl, sigma0[l], sigma1[l], dpt0[l], dpt1[l],
+                                     m0[l], m1[l])
+                out = TS.uic_solve(pose, lv, tr.max_iterations, want_jtj=self.uncer_prop)
+                if self.uncer_prop:
+                    sig.append(out[1])
+            pose = out[0]
+            poses[0].append(pose[0])
+            poses[1].append(pose[1])
+        pyr_R, pyr_t = torch.stack(poses[0], dim=1), torch.stack(poses[1], dim=1)
+        return (pyr_R, pyr_t, torch.stack(sig, dim=1)) if self.uncer_prop else (pyr_R, pyr_t)
+
     def compute_residual(self, img0, img1, depth0, depth1, K, poseI=None, level_i=0, logger=None, vis=False,
                          obj_mask0=None, obj_mask1=None):
         """Residual-only loss at `level_i` for pose `poseI` (LeastSquareTracking.py:605-651)."""
@@ -224,6 +261,15 @@ class LeastSquareTracking(nn.Module):
         (I0, I1, x0, x1, sigma0, sigma1, dpt0, dpt1, inv_d0, inv_d1, m0, m1, _) = prepared
         i = level_i
         tr = self.tr_update0
+        if TS.needs_torch_path(x0[i]):  # CPU tensors: one residual evaluation per pose
+            Ki = K / float(1 << i)
+            if self.track_type == 'IC':
+                return torch.stack([tr.forward_residuals([R[p], t[p].reshape(-1, 3, 1)], x0[i], x1[i], inv_d0[i],
+                                                         inv_d1[i], Ki, torch.ones_like(inv_d0[i]), obj_mask0=m0[i],
+                                                         obj_mask1=m1[i]) for p in range(R.shape[0])])
+            return torch.stack([tr.forward_residuals([R[p], t[p].reshape(-1, 3, 1)], x0[i], x1[i], inv_d0[i], inv_d1[i],
+                                                     Ki, sigma0[i], sigma1[i], depth0=dpt0[i], depth1=dpt1[i],
+                                                     obj_mask0=m0[i], obj_mask1=m1[i]) for p in range(R.shape[0])])
         if self.track_type == 'IC':
             if tr._learned_weights():
                 raise NotImplementedError("the multi-pose residual sweep uses unit weights; with a learned "
@@ -299,7 +345,7 @@ class LeastSquareTracking(nn.Module):
             dp0 = dp1 = None
         I0 = color_normalize(img0)
         I1 = color_normalize(img1)
-        with torch.no_grad():
+        with (contextlib.nullcontext() if self.training else torch.no_grad()):  # training: through the encoder
             x0, sigma0, orig_x0 = self._encode(I0, invD0, I1, invD1)
             x1, sigma1, orig_x1 = self._encode(I1, invD1, I0, invD0)
         if self.combine_icp:
@@ -311,7 +357,7 @@ class LeastSquareTracking(nn.Module):
         m1 = self.construct_image_pyramids(obj_mask1) if obj_mask1 is not None else [None] * len(self.scales)
         if poseI is None:
             if self.predict_init_pose:
-                with torch.no_grad():
+                with (contextlib.nullcontext() if self.training and self.train_init_pose else torch.no_grad()):
                     R0, t0 = self.pose_predictor(orig_x0[3], orig_x1[3])
             else:
                 B = invD0.shape[0]

@@ -2,10 +2,12 @@
 
 `TrustRegionInverseWUncertainty` is the drop-in for the reference's class of the
 same name (code/models/algorithms.py:579-997): same constructor, same
-`forward` / `forward_residuals` signatures and return values, but every level
-runs through libdpft_ic.so (deep_prob_feature_track_amd.ic).  There is no
-PyTorch fallback: configurations the kernels do not implement raise
-NotImplementedError, CPU tensors raise RuntimeError.
+`forward` / `forward_residuals` signatures and return values.  Device tensors at
+inference run every level through libdpft_ic.so (deep_prob_feature_track_amd.ic), which
+fails loudly when it is missing; CPU tensors and calls with gradients (grad enabled and an
+input that requires grad: the reference's training path) take the PyTorch path of
+torch_solver.py (SURVEY.md 8(b)'s dispatch rule).  Configurations neither implements
+raise NotImplementedError.
 
 The networks around it (feature encoder, pose initialisers, estimator
 networks of the IC tracker) are PyTorch modules whose parameter names match the
@@ -23,6 +25,7 @@ import torch.nn.functional as func
 from .. import ic
 from .. import torch_ops  # noqa: F401  (registers the dpft:: ops torch.compile traces)
 from . import geometry
+from . import torch_solver as TS
 from .submodules import convLayer as conv
 from .submodules import convLayer1d as conv1d
 from .submodules import fcLayer, initialize_weights
@@ -426,9 +429,6 @@ class TrustRegionBase(nn.Module):
         self.directSolver = solver_func
         self.timers = timers
 
-    def _check(self, x0):
-        if torch.is_grad_enabled() and x0.requires_grad:
-            raise NotImplementedError("the HIP IC solver is inference-only (no backward kernels)")
 
     def _learned_weights(self):
         return self.mEstimator is not None and getattr(self.mEstimator, 'D', -1) > 0
@@ -439,6 +439,8 @@ class TrustRegionBase(nn.Module):
         = 1 and a zero residual (its a = -gx / sigma, J = -(a Jx + b Jy)).  The fused
         iteration never builds it."""
         B, C, H, W = x.shape
+        if TS.needs_torch_path(x, invD):  # CPU tensors / gradients
+            return TS.ic_template_jacobian(invD, x, px.expand(B, -1, -1, -1), py.expand(B, -1, -1, -1), K.reshape(B, 4))
         g = ic.feature_gradient(x)
         Jx_p, Jy_p = ic.warp_jacobian(invD, K, px, py)
         one = torch.ones((1, 1, 1, 1), dtype=torch.float32, device=x.device).expand(B, C, H, W)
@@ -449,8 +451,10 @@ class TrustRegionBase(nn.Module):
 
     def GN_solver(self, JtJ, JtR, pose0):
         """lev_mar_H + inverse_update_pose (algorithms.py:105-107, 2094-2103, 2017-2054) in
-        one launch (dpft_ic_damped_update)."""
+        one launch (dpft_ic_damped_update); the PyTorch path for CPU tensors / gradients."""
         B = JtJ.shape[0]
+        if TS.needs_torch_path(JtJ, JtR, *pose0):
+            return TS.damped_update(JtJ, JtR, pose0)
         R, t = ic.damped_update(JtJ, JtR.reshape(B, 6), None, pose0)
         return [R[0], t[0]]
 
@@ -464,7 +468,8 @@ class TrustRegionBase(nn.Module):
         return self.mEstimator(res, x0, x1, wPrior), res, occ
 
     def forward(self, pose, x0, x1, invD0, invD1, K, wPrior=None, vis_res=False, obj_mask0=None, obj_mask1=None):
-        self._check(x0)
+        if TS.needs_torch_path(x0, x1, invD0, invD1, *pose):  # CPU tensors / gradients
+            return TS.ic_forward(self, pose, x0, x1, invD0, invD1, K, wPrior, obj_mask0, obj_mask1)
         B, C, H, W = x0.shape
         resvol = getattr(self.directSolver, 'type', 0) == DirectSolverNet.SOLVER_RESIDUAL_VOLUME
         with torch.no_grad():
@@ -492,7 +497,8 @@ class TrustRegionBase(nn.Module):
         """loss [B] (algorithms.py:125-139): the unit-weight loss in one HIP launch, or
         with a learned estimator compute_avg_loss([weights * r], occ) (2119-2137) on the
         HIP residual map."""
-        self._check(x0)
+        if TS.needs_torch_path(x0, x1, invD0, invD1, *pose):  # CPU tensors / gradients
+            return TS.ic_loss(self, pose, x0, x1, invD0, invD1, K, wPrior, obj_mask0, obj_mask1)
         with torch.no_grad():
             if not self._learned_weights():
                 return ic.residual_level(pose, x0, x1, invD0, invD1, K, None, None, no_uncertainty=True,
@@ -530,10 +536,16 @@ class TrustRegionInverseWUncertainty(nn.Module):
         self.remove_tru_sigma = remove_tru_sigma
 
     def _check_path(self, x0):
-        if torch.is_grad_enabled() and x0.requires_grad:
-            raise NotImplementedError("the HIP U_IC solver is inference-only (no backward kernels)")
         if self.combine_icp and self.scale_func is not None and getattr(self.scale_func, 'D', -1) > 0:
             raise NotImplementedError("learned ICP scalers are not supported by the fused HIP solver")
+
+    def _torch_level(self, x0, x1, invD0, invD1, K, sigma0, sigma1, depth0, depth1, obj_mask0, obj_mask1):
+        """The level for the PyTorch path (CPU tensors / gradients, torch_solver.py)."""
+        if self.combine_icp:
+            assert depth0 is not None and depth1 is not None
+        return TS.UICLevel(x0, x1, invD0, invD1, K, sigma0, sigma1, depth0, depth1, obj_mask0, obj_mask1,
+                           remove_tru_sigma=bool(self.remove_tru_sigma),
+                           icp_scale=self._icp_scale() if self.combine_icp else None)
 
     def _icp_scale(self):
         return float(self.scale_func.scale) if self.scale_func is not None else 0.01
@@ -548,7 +560,7 @@ class TrustRegionInverseWUncertainty(nn.Module):
     def forward(self, pose10, x0, x1, invD0, invD1, K, sigma0, sigma1, wPrior=None,
                 depth0=None, depth1=None, vis_res=True, obj_mask0=None, obj_mask1=None):
         out = self.solve(pose10, x0, x1, invD0, invD1, K, sigma0, sigma1, depth0, depth1, obj_mask0, obj_mask1)
-        if self._deferred_status is None:
+        if self._deferred_status is None and out[3] is not None:
             ic.check_status(out[3])
         return out[:3] if self.uncer_prop else out[:2]
 
@@ -556,10 +568,20 @@ class TrustRegionInverseWUncertainty(nn.Module):
               obj_mask1=None):
         """-> (pose [R, t], weights, JtWJ or None, status [1] int32 device word): forward
         without the host check.  Traced by torch.compile it is one dpft::ic_solve_level op
-        (torch_ops.py); eager, the same library call through ctypes."""
+        (torch_ops.py); eager, the same library call through ctypes.  CPU tensors and calls
+        with gradients take the PyTorch path (status None: it raises AssertionError itself on
+        a non-finite residual or Jacobian, as the reference's asserts do)."""
         assert sigma0 is not None and sigma1 is not None
         self._check_path(x0)
         B, C, H, W = ic.feature_shape(x0)  # NCHW, or the channel-quad layout of a packed encoder
+        if TS.needs_torch_path(x0, x1, invD0, invD1, sigma0, sigma1, *pose10):
+            lv = self._torch_level(x0, x1, invD0, invD1, K, sigma0, sigma1, depth0, depth1, obj_mask0, obj_mask1)
+            pose, jtj = TS.uic_solve(pose10, lv, self.max_iterations, want_jtj=self.uncer_prop)
+            if self.combine_icp:
+                weights = torch.full((1, 1, 1, 1), self._icp_scale(), dtype=x0.dtype, device=x0.device).expand(B, 1, H, W)
+            else:
+                weights = torch.ones((1, 1, 1, 1), dtype=x0.dtype, device=x0.device).expand(B, C, H, W)
+            return pose, weights, jtj, None
         kw = self._common(x0, depth0, depth1, obj_mask0, obj_mask1)
         with torch.no_grad():
             if torch.compiler.is_compiling():
@@ -588,6 +610,10 @@ class TrustRegionInverseWUncertainty(nn.Module):
         if grad_interp:
             raise NotImplementedError("bilinear-interpolation gradients (grad_interp) belong to the forward "
                                       "direction; the inverse path linearises at the origin")
+        if TS.needs_torch_path(f0, sigma0, invD0):  # CPU tensors / gradients
+            B = f0.shape[0]
+            Jx_p, Jy_p = TS.warp_jacobian(px.expand(B, -1, -1, -1), py.expand(B, -1, -1, -1), invD0, K.reshape(B, 4))
+            return torch.stack(TS.sobel(f0), 2), torch.stack(TS.sobel(sigma0), 2), Jx_p, Jy_p
         grad_f0 = ic.feature_gradient(f0)
         if sigma0.shape[1] != 1 and sigma0.stride(1) == 0:  # channel broadcast: one plane's gradient
             grad_sigma0 = ic.feature_gradient(sigma0[:, :1]).expand(-1, sigma0.shape[1], -1, -1, -1)
@@ -600,7 +626,13 @@ class TrustRegionInverseWUncertainty(nn.Module):
         """(J [B,C,HW,6], J_res_trs [B,C,3,H,W], J_res_rot) -- algorithms.py:867-887; the
         two parts are of -J, the chained derivative before the reference's sign flip."""
         B, C, H, W = sigma0.shape
-        J = ic.inverse_jacobian(res, sigma, sigma0, grad_f0, grad_sigma0, Jx_p, Jy_p)
+        if TS.needs_torch_path(res, sigma, sigma0, grad_f0):  # CPU tensors / gradients
+            k = res * sigma0 / sigma ** 3
+            a = -(grad_f0[:, :, 0] / sigma + k * grad_sigma0[:, :, 0])
+            b = -(grad_f0[:, :, 1] / sigma + k * grad_sigma0[:, :, 1])
+            J = -(a.reshape(B, C, -1, 1) * Jx_p.view(B, 1, -1, 6) + b.reshape(B, C, -1, 1) * Jy_p.view(B, 1, -1, 6))
+        else:
+            J = ic.inverse_jacobian(res, sigma, sigma0, grad_f0, grad_sigma0, Jx_p, Jy_p)
         J_res_rot, J_res_trs = (-J).view(B, C, H, W, 6).split(3, dim=-1)
         if not torch.isfinite(J).all():
             raise AssertionError("non-finite Jacobian (reference: assert check_nan(J_res_p) == 0)")
@@ -613,21 +645,32 @@ class TrustRegionInverseWUncertainty(nn.Module):
         if direction != 'inverse':
             raise NotImplementedError("the forward-compositional update belongs to the U_FC tracker")
         B = JtJ.shape[0]
+        if TS.needs_torch_path(JtJ, JtR, *pose0):
+            return TS.damped_update(JtJ, JtR, pose0)
         R, t = ic.damped_update(JtJ, JtR.reshape(B, 6), None, pose0)
         return [R[0], t[0]]
 
     def compute_jtj(self, jac):
         """J [B,C,HW,6] -> JtJ [B,6,6] (algorithms.py:812-820)."""
+        if TS.needs_torch_path(jac):
+            Jf = jac.reshape(jac.shape[0], -1, 6)
+            return torch.bmm(Jf.transpose(1, 2), Jf)
         return ic.normal_equations(jac)[0]
 
     def compute_jtr(self, jac, res):
         """J [B,C,HW,6], res [B,C,H,W] -> JtR [B,6,1] (algorithms.py:822-834)."""
+        if TS.needs_torch_path(jac, res):
+            Jf = jac.reshape(jac.shape[0], -1, 6)
+            return torch.bmm(Jf.transpose(1, 2), res.reshape(jac.shape[0], -1, 1))
         return ic.normal_equations(jac, res)[1]
 
     def forward_residuals(self, pose10, x0, x1, invD0, invD1, K, sigma0, sigma1, wPrior=None,
                           depth0=None, depth1=None, vis_res=True, obj_mask0=None, obj_mask1=None):
         assert sigma0 is not None and sigma1 is not None
         self._check_path(x0)
+        if TS.needs_torch_path(x0, x1, invD0, invD1, sigma0, sigma1, *pose10):
+            lv = self._torch_level(x0, x1, invD0, invD1, K, sigma0, sigma1, depth0, depth1, obj_mask0, obj_mask1)
+            return lv.loss(pose10)
         kw = self._common(x0, depth0, depth1, obj_mask0, obj_mask1)
         with torch.no_grad():
             if torch.compiler.is_compiling():

@@ -228,7 +228,12 @@ int dpft_ic_residual_map(const DpftLevelDesc* desc, const DpftLevelTensors* tens
 
 /* Kernel-only timing hook for the roofline: launch ONLY the fused residual +
  * Jacobian + normal-equation kernel (no finalize), using the sigma0 extrema a
- * previous dpft_ic_iterate(first=1) left in the workspace.  Used by bench.py. */
+ * previous dpft_ic_iterate(first=1) left in the workspace.  Used by tools/kbench.py.
+ * With DPFT_COMBINE_ICP on the channel-quad path (DPFT_FEATURES_C4, C % 16 == 0) this is
+ * TWO launches -- the point-to-plane pass (icp_records_kernel) and the U_IC reduce -- and
+ * the per-workgroup records it leaves hold the U_IC terms only: the ICP records are merged
+ * by the finalize (pair_reduce2), which this hook does not run.  Timing only: its records
+ * are not the level's normal equations on that path. */
 int dpft_ic_reduce_only(const DpftLevelDesc* desc, const DpftLevelTensors* tensors,
                         const float* R, const float* t,
                         void* workspace, size_t workspace_bytes, void* hip_stream);

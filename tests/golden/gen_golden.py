@@ -4,6 +4,7 @@ Run in the build container only (needs /root/reference; refuses otherwise):
 
     PYTHONDONTWRITEBYTECODE=1 python tests/golden/gen_golden.py [case ...]
     PYTHONDONTWRITEBYTECODE=1 python tests/golden/gen_golden.py --noise case ...   (noise-floor runs)
+    PYTHONDONTWRITEBYTECODE=1 python tests/golden/gen_golden.py --noise-more=N case ...   (N more such runs)
 
 No reference code is copied: the reference package is imported read-only from
 /root/reference/code with the import shims of SURVEY.md Appendix A (stub
@@ -59,6 +60,8 @@ OPTIONS = {
     "cfg2_640x480_c32": dict(remove_tru_sigma=True, combine_icp=False),
     "icp_640x480_c32": dict(remove_tru_sigma=True, combine_icp=True),
     "cfg3_b8_640x480_c32": dict(remove_tru_sigma=True, combine_icp=False),
+    "cfg3_b8q2_640x480_c32": dict(remove_tru_sigma=True, combine_icp=False),
+    "cfg3_b8q7_640x480_c32": dict(remove_tru_sigma=True, combine_icp=False),
     "cfg4_pert00_160x120_c8": dict(remove_tru_sigma=True, combine_icp=False),
     "cfg4_pert05_160x120_c8": dict(remove_tru_sigma=True, combine_icp=False),
     "cfg4_pert10_160x120_c8": dict(remove_tru_sigma=True, combine_icp=False),
@@ -66,6 +69,8 @@ OPTIONS = {
     "cfg4_sweep256_160x120_c8": dict(remove_tru_sigma=True, combine_icp=False),
     "cfg4_sweep256_rotx10_160x120_c8": dict(remove_tru_sigma=True, combine_icp=False),
     "cfg4_sweep256_tz10_160x120_c8": dict(remove_tru_sigma=True, combine_icp=False),
+    "cfg4_sweep256_ry011_160x120_c8": dict(remove_tru_sigma=True, combine_icp=False),
+    "cfg4_sweep256_tz012_160x120_c8": dict(remove_tru_sigma=True, combine_icp=False),
 }
 
 
@@ -88,8 +93,8 @@ def import_reference():
     return torch, A
 
 
-def run_case(torch, A, name, dtype, perturb_first=None):
-    """perturb_first: (numpy Generator, amplitude) -- every update's pose moved by fresh
+def run_case(torch, A, name, dtype, perturb_updates=None):
+    """perturb_updates: (numpy Generator, amplitude) -- every update's pose moved by fresh
     uniform noise of that amplitude (the --noise / --noise64 runs); None: the plain run."""
     spec = recipe.CASES[name]
     opt = OPTIONS[name]
@@ -99,12 +104,12 @@ def run_case(torch, A, name, dtype, perturb_first=None):
     if dtype == torch.float64:  # the mask sampling of algorithms.py:2006 (see the module docstring)
         G.warp_features = lambda F, u, v: orig_wf(F.to(u.dtype), u, v)
     try:
-        return _run_case(torch, A, name, dtype, spec, opt, case, perturb_first)
+        return _run_case(torch, A, name, dtype, spec, opt, case, perturb_updates)
     finally:
         G.warp_features = orig_wf
 
 
-def _run_case(torch, A, name, dtype, spec, opt, case, perturb_first=None):
+def _run_case(torch, A, name, dtype, spec, opt, case, perturb_updates=None):
     L = case["levels"]
     B, C = case["B"], case["C"]
     tt = lambda a: torch.from_numpy(np.ascontiguousarray(a)).to(dtype)
@@ -133,8 +138,8 @@ def _run_case(torch, A, name, dtype, spec, opt, case, perturb_first=None):
 
             def gn(JtJ, JtR, pose0, direction="inverse", _o=orig_gn):
                 out = _o(JtJ, JtR, pose0)
-                if perturb_first is not None:  # every update moved by fresh U(+-amplitude) noise
-                    rng, amp = perturb_first
+                if perturb_updates is not None:  # every update moved by fresh U(+-amplitude) noise
+                    rng, amp = perturb_updates
                     dR = torch.from_numpy(rng.uniform(-amp, amp, size=tuple(out[0].shape))).to(out[0].dtype)
                     dt = torch.from_numpy(rng.uniform(-amp, amp, size=tuple(out[1].shape))).to(out[1].dtype)
                     out = [out[0] + dR, out[1] + dt]
@@ -193,17 +198,30 @@ def _run_case(torch, A, name, dtype, spec, opt, case, perturb_first=None):
 NOISE_TRIALS, JITTER_ABS = 8, 3.4e-8
 
 
-def add_noise_floor(torch, A, name):
+def add_noise_floor(torch, A, name, append=0):
     """The reference's own fp32 noise floor of a case (see the module docstring): appends
     f32_jitter_R [N, iters, B, 3, 3] / f32_jitter_t [N, iters, B, 3] (every iteration of
-    NOISE_TRIALS jittered-start runs) and f32_t1_R / f32_t1_t [iters, B, ...] (the
-    unjittered run on one thread) to the case's fixture."""
+    NOISE_TRIALS runs in which every Gauss-Newton update's R and t are moved by fresh
+    U(+-JITTER_ABS) noise) and f32_t1_R / f32_t1_t [iters, B, ...] (the unperturbed run on
+    one thread) to the case's fixture."""
     path = os.path.join(HERE, f"{name}.npz")
     out = dict(np.load(path, allow_pickle=False))
+    if append:  # more runs of the same kind (fresh seeds) beside the existing ones
+        n0 = out["f32_jitter_R"].shape[0]
+        rng = np.random.default_rng(1000 * n0 + sum(ord(c) for c in name))
+        Rs, ts = list(out["f32_jitter_R"]), list(out["f32_jitter_t"])
+        for _ in range(append):
+            _, res = run_case(torch, A, name, torch.float32, perturb_updates=(rng, JITTER_ABS))
+            Rs.append(res["R"])
+            ts.append(res["t"])
+        out["f32_jitter_R"], out["f32_jitter_t"] = np.stack(Rs), np.stack(ts)
+        np.savez_compressed(path, **out)
+        print(f"{name}: {len(Rs)} per-update jitter runs", flush=True)
+        return
     rng = np.random.default_rng(sum(ord(c) for c in name))
     Rs, ts = [], []
     for _ in range(NOISE_TRIALS):
-        _, res = run_case(torch, A, name, torch.float32, perturb_first=(rng, JITTER_ABS))
+        _, res = run_case(torch, A, name, torch.float32, perturb_updates=(rng, JITTER_ABS))
         Rs.append(res["R"])
         ts.append(res["t"])
     nthreads = torch.get_num_threads()
@@ -219,7 +237,7 @@ def add_noise_floor(torch, A, name):
     dev = max(np.abs(out["f32_jitter_R"][:, -1] - out["f32_R"][-1]).max(),
               np.abs(out["f32_jitter_t"][:, -1] - out["f32_t"][-1]).max())
     dev1 = max(np.abs(res1["R"][-1] - out["f32_R"][-1]).max(), np.abs(res1["t"][-1] - out["f32_t"][-1]).max())
-    print(f"{name}: reference final pose moves by up to {dev:.2e} under {JITTER_ABS:g} start jitter, "
+    print(f"{name}: reference final pose moves by up to {dev:.2e} under {JITTER_ABS:g} per-update jitter, "
           f"{dev1:.2e} on one thread")
 
 
@@ -227,15 +245,15 @@ NOISE64_ABS = 1e-16
 
 
 def add_noise_floor64(torch, A, name):
-    """The reference's fp64 noise floor (NOISE_TRIALS fp64 runs, start translation moved by
-    U(+-NOISE64_ABS): the truncated-sigma equality tests flip pixels in fp64 too): appends
-    f64_jitter_R / f64_jitter_t [N, iters, B, ...]."""
+    """The reference's fp64 noise floor (NOISE_TRIALS fp64 runs in which every update's R and
+    t are moved by fresh U(+-NOISE64_ABS) noise: the truncated-sigma equality tests flip
+    pixels in fp64 too): appends f64_jitter_R / f64_jitter_t [N, iters, B, ...]."""
     path = os.path.join(HERE, f"{name}.npz")
     out = dict(np.load(path, allow_pickle=False))
     rng = np.random.default_rng(7 + sum(ord(c) for c in name))
     Rs, ts = [], []
     for _ in range(NOISE_TRIALS):
-        _, res = run_case(torch, A, name, torch.float64, perturb_first=(rng, NOISE64_ABS))
+        _, res = run_case(torch, A, name, torch.float64, perturb_updates=(rng, NOISE64_ABS))
         Rs.append(res["R"])
         ts.append(res["t"])
     out["f64_jitter_R"], out["f64_jitter_t"] = np.stack(Rs), np.stack(ts)
@@ -243,7 +261,7 @@ def add_noise_floor64(torch, A, name):
     np.savez_compressed(path, **out)
     dev = max(np.abs(out["f64_jitter_R"][:, -1] - out["f64_R"][-1]).max(),
               np.abs(out["f64_jitter_t"][:, -1] - out["f64_t"][-1]).max())
-    print(f"{name}: fp64 reference final pose moves by up to {dev:.2e} under {NOISE64_ABS:g} start jitter", flush=True)
+    print(f"{name}: fp64 reference final pose moves by up to {dev:.2e} under {NOISE64_ABS:g} per-update jitter", flush=True)
 
 
 def main(names):
@@ -255,6 +273,11 @@ def main(names):
     if names and names[0] == "--noise":
         for name in names[1:]:
             add_noise_floor(torch, A, name)
+        return
+    if names and names[0].startswith("--noise-more="):  # --noise-more=N case ...: N more runs each
+        n = int(names[0].split("=", 1)[1])
+        for name in names[1:]:
+            add_noise_floor(torch, A, name, append=n)
         return
     nthreads = torch.get_num_threads()
     for name in names:

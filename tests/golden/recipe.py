@@ -205,6 +205,14 @@ def sweep_spec(B, C=8, levels=4, base_down=4, masks=True):
                 base_down=base_down, masks=masks, flips=[(k // len(ORDERED_PAIRS)) % 4 for k in range(B)])
 
 
+def stream_batch_spec(q, B=8, C=32, levels=4, base_down=1):
+    """Batch q of bench.py's cfg3 eval stream: stream pairs q B .. q B + B - 1, stream pair n
+    = ordered pair n mod 20 with flip code (n div 20) mod 4 (bench.make_batches)."""
+    n = [q * B + k for k in range(B)]
+    return dict(pairs=[ORDERED_PAIRS[i % len(ORDERED_PAIRS)] for i in n], C=C, levels=levels, base_down=base_down,
+                flips=[(i // len(ORDERED_PAIRS)) % 4 for i in n])
+
+
 INPUT_KEYS_PREFIX = ("x0_", "x1_", "s0_", "s1_", "invD0_", "invD1_", "depth0_", "depth1_", "mask0_", "mask1_")
 
 
@@ -263,9 +271,19 @@ CASES = {
     "cfg4_pert20_160x120_c8": dict(pairs=CFG4_PAIRS, C=8, levels=4, base_down=4, masks=True,
                                    init=perturbations(4, 0.20, 0.15, 2)),
 }
+# cfg3: two more batches of the bench's stream, with the flips the unflipped batch 0 lacks --
+# batch 2 (stream pairs 16-23: flip codes 0 and 1) and batch 7 (pairs 56-63: codes 2 and 3)
+CASES["cfg3_b8q2_640x480_c32"] = stream_batch_spec(2)
+CASES["cfg3_b8q7_640x480_c32"] = stream_batch_spec(7)
 # cfg4's full batch: 256 masked pairs (80 distinct: the 20 ordered pairs x 4 flip codes), identity start
 CASES["cfg4_sweep256_160x120_c8"] = sweep_spec(256)
 # cfg4's batch from two perturbed start sets (convergence_basin.py:337-418's 1-D axes applied
 # to the identity start): a 0.1 rad rotation about x, a 0.1 m translation along z
 CASES["cfg4_sweep256_rotx10_160x120_c8"] = dict(sweep_spec(256), init=[([0.1, 0.0, 0.0], [0.0, 0.0, 0.0])] * 256)
 CASES["cfg4_sweep256_tz10_160x120_c8"] = dict(sweep_spec(256), init=[([0.0, 0.0, 0.0], [0.0, 0.0, 0.1])] * 256)
+# ... and two start sets INSIDE the basin's decision band: offsets at which the reference's own
+# solve brings part of the batch back within 0.01 rad / 0.01 m of the identity-start solve and
+# leaves the rest outside (its count strictly between 0 and B: 0.011 rad about y, 0.012 m along
+# z), so an exact count comparison can fail
+CASES["cfg4_sweep256_ry011_160x120_c8"] = dict(sweep_spec(256), init=[([0.0, 0.011, 0.0], [0.0, 0.0, 0.0])] * 256)
+CASES["cfg4_sweep256_tz012_160x120_c8"] = dict(sweep_spec(256), init=[([0.0, 0.0, 0.0], [0.0, 0.0, 0.012])] * 256)

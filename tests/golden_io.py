@@ -46,25 +46,54 @@ def init_pose(case, dtype=torch.float32, device="cpu"):
     return R, t
 
 
-def noise_floor(z, prec="f32"):
-    """The reference's own `prec` noise floor per iteration, [iters, B] (None if the
-    fixture has none): how far its trajectory moves when only rounding changes -- max over
-    the jittered-start runs (start translation moved by U(+-3.4e-8), the measured one-step
-    deviation of the HIP solve from the reference) and the one-thread run of max(|dR|, |dt|)
-    against the fixture's fp32 run (tests/golden/gen_golden.py --noise); prec="f64": the
-    fp64 jittered-start runs (start moved by U(+-1e-15), --noise64)."""
+def noise_runs(z, prec="f32"):
+    """The reference's own rounding-only runs of a fixture, (R [N, iters, B, 3, 3],
+    t [N, iters, B, 3]) or None: the --noise runs in which every Gauss-Newton update's R
+    and t were moved by fresh U(+-3.4e-8) noise (the measured one-step deviation of the HIP
+    solve from the reference), plus the unperturbed run on one thread (fp32); prec="f64":
+    the --noise64 runs (every update moved by U(+-1e-16))."""
     if f"{prec}_jitter_R" not in z:
         return None
-    R, t = z[f"{prec}_R"], z[f"{prec}_t"]
-    dR = np.abs(z[f"{prec}_jitter_R"] - R[None]).max(axis=(0, 3, 4))
-    dt = np.abs(z[f"{prec}_jitter_t"] - t[None]).max(axis=(0, 3))
-    fl = np.maximum(dR, dt)
+    Rs, ts = z[f"{prec}_jitter_R"], z[f"{prec}_jitter_t"]
     if prec == "f32" and "f32_t1_R" in z:
-        fl = np.maximum(fl, np.maximum(np.abs(z["f32_t1_R"] - R).max(axis=(2, 3)), np.abs(z["f32_t1_t"] - t).max(axis=2)))
-    # per iteration, the largest move of any pair: which pair a rounding change hits is itself
-    # chance (the batch-global sigma_r extrema sit in one pair's pixels; B = 256 shows it: the
-    # trials move a few pairs each, different ones), so the floor is the batch's, not a pair's
-    return np.broadcast_to(fl.max(axis=1, keepdims=True), fl.shape).copy()
+        Rs = np.concatenate([Rs, z["f32_t1_R"][None]])
+        ts = np.concatenate([ts, z["f32_t1_t"][None]])
+    return Rs, ts
+
+
+def noise_floor(z, prec="f32"):
+    """The reference's own `prec` noise floor per iteration AND PER PAIR, [iters, B] (None
+    if the fixture has none): how far that pair's trajectory moves when only rounding
+    changes -- the max over the rounding-only runs (noise_runs) of max(|dR|, |dt|) against
+    the fixture's `prec` run.  Each pair is bounded by its own floor (the batch maximum,
+    noise_floor_batch, is a printed diagnostic only)."""
+    runs = noise_runs(z, prec)
+    if runs is None:
+        return None
+    R, t = z[f"{prec}_R"], z[f"{prec}_t"]
+    dR = np.abs(runs[0] - R[None]).max(axis=(0, 3, 4))
+    dt = np.abs(runs[1] - t[None]).max(axis=(0, 3))
+    return np.maximum(dR, dt)
+
+
+def noise_floor_batch(z, prec="f32"):
+    """Per iteration, the largest rounding-only move of any pair of the batch [iters]
+    (diagnostic: which pair a rounding change hits is partly chance -- the batch-global
+    sigma_r extrema sit in one pair's pixels)."""
+    fl = noise_floor(z, prec)
+    return None if fl is None else fl.max(axis=1)
+
+
+def noise_counts_beyond(z, tol, i=-1, prec="f32"):
+    """Per rounding-only run, the number of pairs whose pose at iteration i moved by more
+    than `tol` from the fixture's run [N] (how many pairs the reference itself moves by
+    that much under a change of rounding alone)."""
+    runs = noise_runs(z, prec)
+    if runs is None:
+        return None
+    d = np.maximum(np.abs(runs[0][:, i] - z[f"{prec}_R"][i][None]).max(axis=(2, 3)),
+                   np.abs(runs[1][:, i] - z[f"{prec}_t"][i][None]).max(axis=2))
+    return (d > tol).sum(axis=1)
 
 
 def pose_deviation(R, t, z, prec="f32", i=-1):

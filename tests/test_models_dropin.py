@@ -65,17 +65,17 @@ def _loaded(name, device):
     return m.to(device), T
 
 
-def test_cpu_tensors_have_no_fallback():
-    m, T = _loaded("rgb_identity_masks", "cpu")
-    with pytest.raises(RuntimeError, match="no CPU fallback"):
-        m(T["img0"], T["img1"], T["depth0"], T["depth1"], T["K"])
-
-
-def test_training_mode_forward_raises():
-    m, T = _loaded("rgb_identity_masks", "cpu")
-    m.train()
-    with pytest.raises(NotImplementedError):
-        m(T["img0"], T["img1"], T["depth0"], T["depth1"], T["K"])
+def test_device_solver_without_library_fails_loudly(monkeypatch):
+    """Device tensors at inference never fall back to the PyTorch path: with the library
+    unloadable the HIP solver raises (the CPU / gradient path is tests/test_torch_path.py)."""
+    from deep_prob_feature_track_amd import _native
+    from deep_prob_feature_track_amd.models import torch_solver as TS
+    x = torch.zeros(1, 4, 8, 8)
+    assert TS.needs_torch_path(x)  # CPU tensors: the PyTorch path
+    monkeypatch.setattr(_native, "LIB_PATH", "/nonexistent/libdpft_ic.so")
+    monkeypatch.setattr(_native, "_lib", None)
+    with pytest.raises((OSError, RuntimeError)):
+        _native.lib()
 
 
 @pytest.mark.gpu

@@ -16,8 +16,9 @@ import recipe
 from oracle import ic_oracle as O
 
 CASES = list(recipe.CASES)
-SLOW_F64 = {"cfg3_b8_640x480_c32",  # ~35 s per fp64 oracle run on 8 CPU threads
-            "cfg4_sweep256_160x120_c8", "cfg4_sweep256_rotx10_160x120_c8", "cfg4_sweep256_tz10_160x120_c8"}
+SLOW_F64 = {"cfg3_b8_640x480_c32", "cfg3_b8q2_640x480_c32", "cfg3_b8q7_640x480_c32",  # ~35 s per fp64 run
+            "cfg4_sweep256_160x120_c8", "cfg4_sweep256_rotx10_160x120_c8", "cfg4_sweep256_tz10_160x120_c8",
+            "cfg4_sweep256_ry011_160x120_c8", "cfg4_sweep256_tz012_160x120_c8"}
 
 
 def run_oracle(name, dtype):
@@ -61,18 +62,18 @@ def test_oracle_matches_reference(name, prec):
     L = case["levels"]
     # where the reference itself is more sensitive than `loose` at an iteration (its own
     # trajectory moves by more when only rounding changes: golden_io.noise_floor, per
-    # iteration and pair), a chained trajectory is bounded there by twice that floor; the
-    # restarted test below is exact
+    # iteration and PER PAIR), a chained trajectory is bounded there by 1.5x that pair's own
+    # floor; the restarted test below is exact
     floor = golden_io.noise_floor(z, prec)
     prev_dev = 0.0
     for i, tr in enumerate(trace):
         dR = np.abs(tr["R"].numpy() - z[f"{prec}_R"][i]).max(axis=(1, 2))
         dt = np.abs(tr["t"].numpy() - z[f"{prec}_t"][i]).max(axis=1)
-        tol = tight if i == 0 else np.maximum(loose, 2.0 * floor[i]) if floor is not None else loose
+        tol = tight if i == 0 else np.maximum(loose, 1.5 * floor[i]) if floor is not None else loose
         assert (dR <= tol).all() and (dt <= tol).all(), f"{name} {prec} iter {i}: |dR|={dR.max():.3e} |dt|={dt.max():.3e}"
         over = np.flatnonzero(np.maximum(dR, dt) > 1e-4)
         if over.size:
-            print(f"{name} {prec} iter {i}: pairs beyond 1e-4 (within 2x the reference's noise floor):",
+            print(f"{name} {prec} iter {i}: pairs beyond 1e-4 (within 1.5x their own reference noise floor):",
                   {int(b): f"{max(dR[b], dt[b]):.2e} (floor {floor[i][b]:.2e})" for b in over})
         jtj_ref = z[f"{prec}_jtj"][i]
         rel = np.abs(tr["JtJ"].numpy() - jtj_ref).max() / np.abs(jtj_ref).max()
@@ -83,9 +84,19 @@ def test_oracle_matches_reference(name, prec):
         # Chained, the invalid set drifts with the pose noise (the truncated-sigma equality
         # tests flip pixels under 1e-5 pose changes: measured up to 0.4 % of a level's
         # pixels); the restarted test below proves the counts exact from the same pose.
-        dinv = np.abs(tr["invalid"].numpy() - z[f"{prec}_invalid"][i]).max()
+        # A pair whose chained pose took a rounding branch of the mask (beyond 1e-4 of the
+        # reference, within its own floor above) flips a whole sigma plateau: its count is
+        # reported, not bounded.
+        dinv = np.abs(tr["invalid"].numpy() - z[f"{prec}_invalid"][i])
         npx = case[f"invD0_{L - 1 - i // 3}"][0].size
-        assert dinv == 0 if (i == 0 or not fragile) else dinv <= 0.01 * npx, f"iter {i}: {dinv} of {npx}"
+        if i == 0 or not fragile:
+            assert dinv.max() == 0, f"iter {i}: {dinv.max()} of {npx}"
+        else:
+            on = np.maximum(dR, dt) <= 1e-4
+            assert (dinv[on] <= 0.01 * npx).all(), f"iter {i}: {dinv[on].max()} of {npx}"
+            if (~on).any():
+                print(f"{name} {prec} iter {i}: invalid-count differences of the pairs beyond 1e-4:",
+                      {int(b): int(dinv[b]) for b in np.flatnonzero(~on)})
 
 
 @pytest.mark.parametrize("name", CASES)

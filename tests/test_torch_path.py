@@ -1,0 +1,210 @@
+"""The PyTorch path of the solvers (models/torch_solver.py, SURVEY.md 8(b)'s dispatch rule):
+CPU tensors and calls with gradients, pinned against the reference's own outputs.
+
+* Solver level: the drop-in `TrustRegionInverseWUncertainty` on CPU tensors, level by level
+  as LeastSquareTracking.forward drives it, against the reference solver's fixtures
+  (tests/golden/gen_golden.py): every iteration restarted from the reference's pose gives the
+  invalid-pixel count exactly, J^T J / J^T R and the one-step pose to rounding; the chained
+  solve ends within each pair's bound (max(1e-4, 1.5x its own noise floor)).
+* Module level: the drop-in `LeastSquareTracking` on CPU against the reference module's
+  outputs (tests/golden/gen_model_golden.py), for every configuration, and the reference's
+  `run_example.py` call sequence (run_example.py:84-105) replayed through the `models` alias.
+* Gradients: the solve is differentiable (finite gradients into the features) and equals the
+  no-grad result; training-mode forward returns the stacked per-level poses
+  (LeastSquareTracking.py:568-575) with gradients into the encoder.
+"""
+import os
+import subprocess
+import sys
+
+import numpy as np
+import pytest
+import torch
+
+import golden_io
+import gen_model_golden as G
+import recipe
+from deep_prob_feature_track_amd.models import algorithms as A
+from deep_prob_feature_track_amd.models import torch_solver as TS
+from deep_prob_feature_track_amd.models.LeastSquareTracking import LeastSquareTracking, default_options
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+HERE = os.path.join(ROOT, "tests", "golden")
+SOLVER_CASES = ["cfg1_160x120_c8", "cfg1b_160x120_c8_f04", "batch4_160x120_c8", "masks_160x120_c8",
+                "icp_160x120_c8", "cfg4_pert05_160x120_c8", "cfg4_pert20_160x120_c8"]
+
+
+def _solver(z):
+    return A.TrustRegionInverseWUncertainty(3, combine_icp=bool(z["opt_combine_icp"]), scale_func=A.ScaleNet("None"),
+                                            remove_tru_sigma=bool(z["opt_remove_tru_sigma"]))
+
+
+def _level_args(d, K, l):
+    return dict(x0=d["f0"], x1=d["f1"], invD0=d["invD0"], invD1=d["invD1"], K=K / 2 ** l, sigma0=d["s0"],
+                sigma1=d["s1"], depth0=d.get("depth0"), depth1=d.get("depth1"), obj_mask0=d.get("mask0"),
+                obj_mask1=d.get("mask1"))
+
+
+@pytest.mark.parametrize("name", SOLVER_CASES)
+def test_cpu_solver_matches_reference(name):
+    case, z = golden_io.load(name)
+    lv = golden_io.levels_torch(case)
+    K = torch.from_numpy(case["K"])
+    R0, t0 = golden_io.init_pose(case)
+    tr = _solver(z)
+    L, i = case["levels"], 0
+    with torch.no_grad():
+        for l in reversed(range(L)):  # restarted iterations: exact counts, normal equations to rounding
+            a = _level_args(lv[l], K, l)
+            level = tr._torch_level(a["x0"], a["x1"], a["invD0"], a["invD1"], a["K"], a["sigma0"], a["sigma1"],
+                                    a["depth0"], a["depth1"], a["obj_mask0"], a["obj_mask1"])
+            for _ in range(3):
+                pose = ([torch.from_numpy(z["f32_R"][i - 1]), torch.from_numpy(z["f32_t"][i - 1]).view(-1, 3, 1)]
+                        if i else [R0, t0.view(-1, 3, 1)])
+                JtJ, JtR, inv = level.normal_equations(pose)
+                assert np.array_equal(inv.numpy(), z["f32_invalid"][i]), f"{name} iter {i}"
+                jtj, jtr = z["f32_jtj"][i], z["f32_jtr"][i]
+                assert np.abs(JtJ.numpy() - jtj).max() / np.abs(jtj).max() < 1e-5, f"iter {i} JtJ"
+                assert np.abs(JtR.numpy().reshape(-1, 6) - jtr).max() / np.abs(jtr).max() < 1e-4, f"iter {i} JtR"
+                Rn, tn = TS.damped_update(JtJ, JtR, pose)
+                assert golden_io.pose_deviation(Rn, tn, z, "f32", i).max() < 2e-5, f"iter {i} one step"
+                i += 1
+        pose = [R0, t0.view(-1, 3, 1)]  # the chained solve through the module's forward
+        for l in reversed(range(L)):
+            pose = tr(pose, wPrior=None, vis_res=False, **_level_args(lv[l], K, l))[0]
+    dev = golden_io.pose_deviation(pose[0], pose[1], z, "f32")
+    floor = golden_io.noise_floor(z)
+    bound = np.maximum(1e-4, 1.5 * floor[-1]) if floor is not None else 1e-4
+    assert (dev <= bound).all(), f"{name}: {dev} vs {bound}"
+    # forward_residuals at the level-0 start pose of the reference's run (algorithms.py:725-786)
+    d = lv[0]
+    pose = [torch.from_numpy(z["f32_R"][3 * L - 4]), torch.from_numpy(z["f32_t"][3 * L - 4]).view(-1, 3, 1)] \
+        if L > 1 else [R0, t0.view(-1, 3, 1)]
+    with torch.no_grad():
+        loss = tr.forward_residuals(pose, wPrior=None, vis_res=False, **_level_args(d, K, 0))
+    np.testing.assert_allclose(loss.numpy(), z["f32_loss_start"][-1], rtol=2e-5)
+
+
+def _loaded(name):
+    spec = G.MODEL_CASES[name]
+    m = LeastSquareTracking(spec["encoder"], spec["uncertainty"], 3, spec.get("mest", "None"),
+                            spec.get("solver", "Direct-Nodamping"), options=default_options(**spec["opts"]),
+                            **spec.get("ctor", {}))
+    m.load_state_dict({k: torch.from_numpy(recipe.synthetic_weights(k, v.shape)) for k, v in m.state_dict().items()})
+    m.eval()
+    inp = G.model_inputs(spec["pairs"], spec["masks"])
+    return m, {k: torch.from_numpy(v) for k, v in inp.items()}
+
+
+@pytest.mark.parametrize("name", sorted(G.MODEL_CASES))
+def test_cpu_module_forward_matches_reference(name):
+    """The drop-in module on CPU tensors: forward() poses within 1e-4 of the reference
+    module's, compute_residual() losses to rtol 1e-4, and the multi-pose residual sweep
+    (convergence_basin.py:340-369) equal to the reference's per-pose loop."""
+    m, T = _loaded(name)
+    z = np.load(os.path.join(HERE, f"model_{name}.npz"), allow_pickle=False)
+    kw = dict(obj_mask0=T.get("mask0"), obj_mask1=T.get("mask1"))
+    with torch.no_grad():
+        R, t = m(T["img0"], T["img1"], T["depth0"], T["depth1"], T["K"], **kw)
+        B = R.shape[0]
+        assert np.abs(R.numpy() - z["R"]).max() < 1e-4
+        assert np.abs(t.numpy().reshape(B, 3) - z["t"].reshape(B, 3)).max() < 1e-4
+        _, loss = m.compute_residual(T["img0"], T["img1"], T["depth0"], T["depth1"], T["K"],
+                                     poseI=[torch.from_numpy(z["R"]), torch.from_numpy(z["t"])], level_i=0, **kw)
+        np.testing.assert_allclose(loss.numpy(), z["res_pose_loss"], rtol=1e-4)
+        ident = [torch.eye(3).expand(B, 3, 3).contiguous(), torch.zeros(B, 3, 1)]
+        _, loss2 = m.compute_residual(T["img0"], T["img1"], T["depth0"], T["depth1"], T["K"], poseI=ident,
+                                      level_i=2, **kw)
+        np.testing.assert_allclose(loss2.numpy(), z["res_init_loss"], rtol=1e-4)
+        if m.track_type == "U_IC" or not m.tr_update0._learned_weights():
+            from deep_prob_feature_track_amd import convergence_basin as CB
+            Rp, tp = CB.axis_perturbations(torch.from_numpy(z["R"]), torch.from_numpy(z["t"]).view(B, 3),
+                                           list(z["basin_offsets"]), list(z["basin_offsets"]))
+            prep = m.prepare(T["img0"], T["img1"], T["depth0"], T["depth1"], **kw)
+            got = m.compute_residual_poses(prep, T["K"], Rp, tp, level_i=0).view(6, -1, B).numpy()
+            np.testing.assert_allclose(got, z["basin_loss"][0], rtol=1e-3)
+
+
+_REPLAY = r"""
+import os, sys
+import numpy as np
+import torch
+sys.path[:0] = [os.path.join(sys.argv[1], "tests"), os.path.join(sys.argv[1], "tests", "golden")]
+import models.LeastSquareTracking as ICtracking          # run_example.py:16, through the alias
+import recipe, gen_model_golden as G
+case, enc, unc, mest, solver, kw = sys.argv[2], sys.argv[3], sys.argv[4], sys.argv[5], sys.argv[6], eval(sys.argv[7])
+net = ICtracking.LeastSquareTracking(encoder_name=enc, max_iter_per_pyr=3, mEst_type=mest, solver_type=solver,
+                                     uncertainty_type=unc, direction='inverse', **kw)   # run_example.py:84-92
+if torch.cuda.is_available():                                                          # run_example.py:102-103
+    net.cuda()
+# torch.load(checkpoint)['state_dict'] (run_example.py:105): the checkpoints are absent; the
+# fixture's deterministic weights stand in
+net.load_state_dict({k: torch.from_numpy(recipe.synthetic_weights(k, v.shape)) for k, v in net.state_dict().items()})
+net.eval()                                                                             # run_example.py:44
+spec = G.MODEL_CASES[case]
+batch = [torch.from_numpy(v) for k, v in G.model_inputs(spec["pairs"], False).items()]
+color0, color1, depth0, depth1, K = batch   # check_cuda (train_utils.py:13-26): no GPU, stays on the host
+with torch.no_grad():                                                                  # run_example.py:55-56
+    R, t = net.forward(color0, color1, depth0, depth1, K)
+z = np.load(os.path.join(sys.argv[1], "tests", "golden", f"model_{case}.npz"))
+print("DEV", float(np.abs(R.numpy() - z["R"]).max()), float(np.abs(t.numpy().reshape(-1, 3) - z["t"].reshape(-1, 3)).max()))
+"""
+
+
+@pytest.mark.parametrize("case,enc,unc,mest,solver,kw", [
+    # run_example.py's own constructor (ConvRGBD2, MultiScale2w, Direct-ResVol, the IC tracker;
+    # its options are the drop-in's config defaults = the fixture's select_deepic configuration)
+    ("select_deepic", "ConvRGBD2", "None", "MultiScale2w", "Direct-ResVol", "{}"),
+    # the U_IC configuration of the shipped eval scripts (laplacian uncertainty, 8 channels)
+    ("convrgbd2_c8", "ConvRGBD2", "laplacian", "None", "Direct-Nodamping",
+     "dict(feature_channel=8, uncertainty_channel=1, feature_extract='conv', remove_tru_sigma=True)"),
+])
+def test_run_example_call_sequence_replays_on_cpu(tmp_path, case, enc, unc, mest, solver, kw):
+    """run_example.py's calls (construct -> .cuda() when a GPU is there -> load_state_dict ->
+    eval -> forward under no_grad) in a child interpreter with only PYTHONPATH changed
+    (dropin/sitecustomize.py) and a shadowing `models/` package in its directory, on a host
+    without a visible GPU: the poses land within 1e-4 of the reference module's."""
+    shadow = tmp_path / "models"
+    shadow.mkdir()
+    (shadow / "__init__.py").write_text("raise ImportError('the shadowed package was imported')\n")
+    env = dict(os.environ, PYTHONPATH=os.path.join(ROOT, "dropin"), PYTHONDONTWRITEBYTECODE="1",
+               HIP_VISIBLE_DEVICES="", CUDA_VISIBLE_DEVICES="")
+    r = subprocess.run([sys.executable, "-c", _REPLAY, ROOT, case, enc, unc, mest, solver, kw], cwd=tmp_path, env=env,
+                       capture_output=True, text=True, timeout=600)
+    assert r.returncode == 0, r.stderr[-3000:]
+    dR, dt = (float(x) for x in r.stdout.strip().splitlines()[-1].split()[1:])
+    assert dR < 1e-4 and dt < 1e-4, (dR, dt)
+
+
+def test_gradients_flow_through_the_solve():
+    """Grad enabled with features that require grad: the PyTorch path (the library has no
+    backward kernels) gives the no-grad poses and finite gradients into both feature maps."""
+    case, z = golden_io.load("batch4_160x120_c8")
+    d = golden_io.levels_torch(case)[0]
+    K = torch.from_numpy(case["K"])
+    R0, t0 = golden_io.init_pose(case)
+    tr = _solver(z)
+    args = _level_args(d, K, 0)
+    with torch.no_grad():
+        ref = tr([R0, t0.view(-1, 3, 1)], **args)[0]
+    x0 = d["f0"].clone().requires_grad_(True)
+    x1 = d["f1"].clone().requires_grad_(True)
+    args.update(x0=x0, x1=x1)
+    pose = tr([R0, t0.view(-1, 3, 1)], **args)[0]
+    assert torch.allclose(pose[0], ref[0], atol=1e-6) and torch.allclose(pose[1], ref[1], atol=1e-6)
+    (pose[0].sum() + pose[1].sum()).backward()
+    for g in (x0.grad, x1.grad):
+        assert g is not None and torch.isfinite(g).all() and g.abs().max() > 0
+
+
+def test_training_mode_forward_returns_stacked_level_poses():
+    """Training mode (LeastSquareTracking.py:568-575): per-level poses [B,4,3,3] / [B,4,3,1]
+    (levels 3 .. 0), the last one the tracked pose; a loss on them reaches the encoder."""
+    m, T = _loaded("convrgbd2_c8")
+    m.train()
+    R, t = m(T["img0"], T["img1"], T["depth0"], T["depth1"], T["K"])
+    B = T["img0"].shape[0]
+    assert R.shape == (B, 4, 3, 3) and t.shape == (B, 4, 3, 1)
+    (R[:, -1].sum() + t[:, -1].sum()).backward()
+    grads = [p.grad for p in m.encoder.parameters() if p.grad is not None]
+    assert grads and all(torch.isfinite(g).all() for g in grads) and any(g.abs().max() > 0 for g in grads)

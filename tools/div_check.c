@@ -3,7 +3,11 @@
 // q1 = fma(r,y,q0) must equal RN(a/b) for every float a the kernel divides (|a| <= 2^30; quotients
 // below 2^-25 cannot move a tap, since (q - 1) + 1 rounds to 0 for them either way).
 //   gcc -O3 -ffp-contract=off -o /tmp/div_check tools/div_check.c -lm
-//   /tmp/div_check 0      all 2^32 floats for the bench's eight divisors (~9 min)
+//   /tmp/div_check 0      all 2^32 floats for the twelve verified divisors (~14 min): every level of
+//                         640x480 and 160x120 (W, H = 640 .. 20, 480 .. 15) -- the set the library
+//                         selects div_const for (kVerifiedTapSizes in csrc/dpft_ic.hip); any other
+//                         size takes the IEEE division
+//   /tmp/div_check 3      all 2^32 floats for the four sizes below 80 x 60 only (~5 min)
 //   /tmp/div_check 1      every size n = 2..8192, a stride of 4099 through all floats (~3 min)
 //   /tmp/div_check 2      quick: the eight divisors, a stride of 65537 (tests/test_div_check.py)
 #include <stdio.h>
@@ -34,9 +38,14 @@ long check(float b, uint64_t lo, uint64_t hi, uint64_t step) {
 }
 int main(int argc, char** argv) {
   int mode = atoi(argv[1]);
-  if (mode == 0) {  // exhaustive for the bench divisors
-    float ds[] = {319.5f, 159.5f, 79.5f, 39.5f, 239.5f, 119.5f, 59.5f, 29.5f};
-    for (int k = 0; k < 8; ++k) { long bad = check(ds[k], 0, 1ull<<32, 1); printf("b=%g bad=%ld\n", ds[k], bad); fflush(stdout);}
+  if (mode == 0 || mode == 3) {  // exhaustive for the verified divisors
+    float ds[] = {319.5f, 159.5f, 79.5f, 39.5f, 239.5f, 119.5f, 59.5f, 29.5f, 19.5f, 9.5f, 14.5f, 7.0f};
+    long tot = 0;
+    for (int k = mode == 3 ? 8 : 0; k < 12; ++k) {
+      long bad = check(ds[k], 0, 1ull<<32, 1); tot += bad; printf("b=%g bad=%ld\n", ds[k], bad); fflush(stdout);
+    }
+    printf("exhaustive: total bad %ld\n", tot);
+    return tot != 0;
   } else if (mode == 2) {  // quick
     float ds[] = {319.5f, 159.5f, 79.5f, 39.5f, 239.5f, 119.5f, 59.5f, 29.5f};
     long tot = 0;

@@ -17,7 +17,8 @@ p.add_argument("--level", type=int, default=0)
 p.add_argument("--batch", type=int, default=8)
 p.add_argument("--groups", type=int, default=1, help="independent --batch-pair batches per launch (DPFT_GROUP)")
 p.add_argument("--reps", type=int, default=20)
-p.add_argument("--mode", choices=["reduce", "iterate", "level"], default="reduce",
+p.add_argument("--mode", choices=["reduce", "iterate", "level"], default="reduce",  # (reduce with --icp --c4: the
+               # ICP pass + the U_IC reduce, two kernels; include/dpft_ic.h dpft_ic_reduce_only)
                help="level: the solve's launches at one level (iterations forward, reverse, forward)")
 p.add_argument("--c4", action="store_true", help="channel-quad packed features")
 p.add_argument("--schedule", default=None, help="auto | march | split (channel-quad reduce kernel)")
