@@ -738,38 +738,80 @@ __device__ __forceinline__ IcpTerm icp_pixel(float xr, float yr, float d0, const
 // [B][H][W] x [nx, ny, nz, depth1] (the depth beside its normal for icp_pixel's taps).
 // `dext`: order-encoded (min, max) word pairs, one per independent batch of `group` pairs
 // (DPFT_GROUP; group = B: the call is one batch, the reference's batch-global extrema).
+// One wave per (pair, 62-column strip, run of `rpr` rows), marching down its run: lane l
+// holds column 62 s - 1 + l (clamped: replicate padding) and keeps the vertices of rows
+// y - 1, y, y + 1 in registers, so each depth row is loaded and turned into vertices once
+// per run (one column division per lane, one row division per row) instead of nine
+// vertices -- eighteen divisions, nine loads -- per pixel; the neighbour columns' vertices
+// come from DPP lane shifts (as the marching kernel's Sobel).  The same IEEE operations on
+// the same operands as per-pixel vertices, bit for bit.  Lanes 1 .. 62 store.  (One
+// short-lived wave per pixel row was launch-bound: 375 -> 201 us at level 0 of 128 pairs.)
+// Runs of up to 16 rows, shorter where that leaves fewer than 16 k waves (coarse levels).
+// Every product and sum is rounded as written (no contraction), so the map does not depend
+// on how the compiler schedules this code.
+__host__ __device__ inline int nrm_rows(int B, int H, int W) {
+  const long cols = (long)B * H * ((W + kTileOut - 1) / kTileOut);
+  return (int)(cols >= 16L * 16384 ? 16 : cols >= 2L * 16384 ? cols / 16384 : 2);
+}
 __global__ __launch_bounds__(kThreads) void icp_normals_kernel(const float* __restrict__ depth, const float* __restrict__ K,
                                                                int B, int H, int W, const uint32_t* __restrict__ dext,
                                                                int group, f32x4* __restrict__ nrm) {
+#pragma clang fp contract(off)
+  const int lane = threadIdx.x & 63;
+  const int rpr = nrm_rows(B, H, W);
+  const int strips = (W + kTileOut - 1) / kTileOut, runs = (H + rpr - 1) / rpr;
+  const long unit = (long)blockIdx.x * (kThreads / 64) + (threadIdx.x >> 6);  // (b, run, strip), strip fastest
+  if (unit >= (long)B * runs * strips) return;  // wave-uniform
+  const int s = (int)(unit % strips);
+  const long br = unit / strips;
+  const int b = (int)(br / runs), y0 = (int)(br - (long)b * runs) * rpr, y1 = min(y0 + rpr, H);
   const int HW = H * W;
-  const long i = (long)blockIdx.x * kThreads + threadIdx.x;
-  if (i >= (long)B * HW) return;
-  const int b = (int)(i / HW), pix = (int)(i - (long)b * HW), y = pix / W, x = pix - y * W;
   dext += 2 * (b / group);
+  const float dmin = dec_ord(dext[0]), dmax = dec_ord(dext[1]);
   const float fx = K[4 * b + 0], fy = K[4 * b + 1], cx = K[4 * b + 2], cy = K[4 * b + 3];
   const float* db = depth + (size_t)b * HW;
-  float V[3][3][3];  // [dy][dx][xyz]
+  const int x = s * kTileOut - 1 + lane, xx = min(max(x, 0), W - 1);
+  const bool out = lane >= 1 && lane <= kTileOut && x < W;
+  const float xr = ((float)xx - cx) / fx;
+  // vertices of one row at this lane's column and its two neighbours: [dx][xyz]
+  auto row = [&](int y, float (&V)[3][3]) {
+    const int yy = min(max(y, 0), H - 1);
+    const float dd = db[yy * W + xx];
+    V[1][0] = xr * dd;
+    V[1][1] = (((float)yy - cy) / fy) * dd;
+    V[1][2] = dd;
 #pragma unroll
-  for (int j = 0; j < 3; ++j)
-#pragma unroll
-    for (int k = 0; k < 3; ++k) {
-      const int yy = min(max(y + j - 1, 0), H - 1), xx = min(max(x + k - 1, 0), W - 1);
-      const float dd = db[yy * W + xx];
-      V[j][k][0] = (((float)xx - cx) / fx) * dd;
-      V[j][k][1] = (((float)yy - cy) / fy) * dd;
-      V[j][k][2] = dd;
+    for (int c = 0; c < 3; ++c) {
+      V[0][c] = lane_from_left(V[1][c]);
+      V[2][c] = lane_from_right(V[1][c]);
     }
-  float gx[3], gy[3];
+  };
+  float Vt[3][3], Vm[3][3], Vb[3][3];  // rows y - 1, y, y + 1
+  row(y0 - 1, Vt);
+  row(y0, Vm);
+  for (int y = y0; y < y1; ++y) {
+    row(y + 1, Vb);
+    float gx[3], gy[3];
 #pragma unroll
-  for (int c = 0; c < 3; ++c) {
-    gx[c] = ((V[0][2][c] - V[0][0][c]) + 2.0f * (V[1][2][c] - V[1][0][c])) + (V[2][2][c] - V[2][0][c]);
-    gy[c] = ((V[2][0][c] - V[0][0][c]) + 2.0f * (V[2][1][c] - V[0][1][c])) + (V[2][2][c] - V[0][2][c]);
+    for (int c = 0; c < 3; ++c) {
+      gx[c] = ((Vt[2][c] - Vt[0][c]) + 2.0f * (Vm[2][c] - Vm[0][c])) + (Vb[2][c] - Vb[0][c]);
+      gy[c] = ((Vb[0][c] - Vt[0][c]) + 2.0f * (Vb[1][c] - Vt[1][c])) + (Vb[2][c] - Vt[2][c]);
+    }
+    if (out) {
+      const float n[3] = {gx[1] * gy[2] - gx[2] * gy[1], gx[2] * gy[0] - gx[0] * gy[2], gx[0] * gy[1] - gx[1] * gy[0]};
+      const float mag = sqrtf((n[0] * n[0] + n[1] * n[1]) + n[2] * n[2]) + 1e-8f;
+      const float d = Vm[1][2];
+      nrm[(size_t)b * HW + (size_t)y * W + x] = (d == dmin || d == dmax) ? f32x4{0.0f, 0.0f, 0.0f, d}
+                                                                          : f32x4{n[0] / mag, n[1] / mag, n[2] / mag, d};
+    }
+#pragma unroll
+    for (int k = 0; k < 3; ++k)
+#pragma unroll
+      for (int c = 0; c < 3; ++c) {
+        Vt[k][c] = Vm[k][c];
+        Vm[k][c] = Vb[k][c];
+      }
   }
-  float n[3] = {gx[1] * gy[2] - gx[2] * gy[1], gx[2] * gy[0] - gx[0] * gy[2], gx[0] * gy[1] - gx[1] * gy[0]};
-  const float mag = sqrtf((n[0] * n[0] + n[1] * n[1]) + n[2] * n[2]) + 1e-8f;
-  const float d = db[pix];
-  const bool bad = d == dec_ord(dext[0]) || d == dec_ord(dext[1]);
-  nrm[i] = bad ? f32x4{0.0f, 0.0f, 0.0f, d} : f32x4{n[0] / mag, n[1] / mag, n[2] / mag, d};
 }
 
 // combine_ICP on the channel-quad path: the point-to-plane term's normal equations in a pass
@@ -3195,10 +3237,11 @@ int launch_minmax(const DpftLevelDesc& d, const DpftLevelTensors& tt, void* ws, 
     } else if ((rc = minmax_into(tt.depth1, (size_t)d.B * d.H * d.W, ctrl, word, st))) {
       return rc;
     }
-    const size_t n = (size_t)d.B * d.H * d.W;
+    const int rpr = nrm_rows(d.B, d.H, d.W);
+    const size_t waves = (size_t)d.B * ((d.H + rpr - 1) / rpr) * ((d.W + kTileOut - 1) / kTileOut);
     f32x4* nrm = reinterpret_cast<f32x4*>(static_cast<char*>(ws) + nrm_offset(d));
-    hipLaunchKernelGGL(icp_normals_kernel, dim3((unsigned)((n + kThreads - 1) / kThreads)), dim3(kThreads), 0, st,
-                       tt.depth1, tt.K, d.B, d.H, d.W, ctrl + word, gs, nrm);
+    hipLaunchKernelGGL(icp_normals_kernel, dim3((unsigned)((waves + kThreads / 64 - 1) / (kThreads / 64))),
+                       dim3(kThreads), 0, st, tt.depth1, tt.K, d.B, d.H, d.W, ctrl + word, gs, nrm);
     if ((rc = hip_check("icp_normals_kernel"))) return rc;
   }
   return DPFT_OK;
