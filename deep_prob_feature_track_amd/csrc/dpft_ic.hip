@@ -862,13 +862,26 @@ __global__ __launch_bounds__(kThreads) void icp_records_kernel(IterParams p, flo
     constexpr bool TAB = decltype(table)::value, RC = decltype(rc)::value;
     auto ncx = [&](int x) { return TAB ? nxy[x] : norm_coord(x, cx, fx); };
     auto ncy = [&](int y) { return TAB ? nxy[W + y] : norm_coord(y, cy, fy); };
-    int pix = beg + tid, y = pix / W, x = pix - y * W;  // then advanced by kThreads without a division
-    for (; pix < end; pix += kThreads) {
-      const bool m0 = m0b ? (m0b[pix] != 0) : true;
-      const float d0 = d0b[pix];
-      const IcpGeo g = icp_geo(ncx(x), ncy(y), d0, Rm, tv, fx, fy, cx, cy, H, W, RC ? rsxy : nullptr);
-      const IcpTapXY n{ncx(g.x0), ncx(g.x1), ncy(g.y0), ncy(g.y1)};
-      const IcpTerm ic = icp_term(g, icp_load(g, nd1), n, d0, Rm, !m0, m1b, p.icp_w);
+    // software-pipelined: pixel k + 1's depth0, geometry and normal-map taps are issued
+    // before pixel k's term (two stages, A / B registers alternating: no loop-carried
+    // copies); past the range the loads are clamped to its last pixel and not accumulated
+    if (end <= beg) return;
+    struct Stage {
+      IcpGeo g;
+      IcpTaps q;
+      float d0;
+      bool m0;
+    };
+    auto issue = [&](Stage& S, int pix, int x, int y) {
+      const int pc = min(pix, end - 1);
+      S.m0 = m0b ? (m0b[pc] != 0) : true;
+      S.d0 = d0b[pc];
+      S.g = icp_geo(ncx(x), ncy(min(y, H - 1)), S.d0, Rm, tv, fx, fy, cx, cy, H, W, RC ? rsxy : nullptr);
+      S.q = icp_load(S.g, nd1);
+    };
+    auto term = [&](const Stage& S) {
+      const IcpTapXY n{ncx(S.g.x0), ncx(S.g.x1), ncy(S.g.y0), ncy(S.g.y1)};
+      const IcpTerm ic = icp_term(S.g, S.q, n, S.d0, Rm, !S.m0, m1b, p.icp_w);
       int kq = 0;
 #pragma unroll
       for (int i = 0; i < 6; ++i) {
@@ -877,11 +890,29 @@ __global__ __launch_bounds__(kThreads) void icp_records_kernel(IterParams p, flo
       }
 #pragma unroll
       for (int i = 0; i < 6; ++i) acc[21 + i] += ic.J[i] * ic.r;
+    };
+    auto advance = [&](int& pix, int& x, int& y) {
+      pix += kThreads;
       x += kThreads;
       while (x >= W) {
         x -= W;
         ++y;
       }
+    };
+    int pix = beg + tid, y = pix / W, x = pix - y * W;  // then advanced by kThreads without a division
+    Stage A, Bs;
+    issue(A, pix, x, y);
+    for (;;) {
+      const int pa = pix;
+      advance(pix, x, y);
+      issue(Bs, pix, x, y);
+      if (pa < end) term(A);
+      if (pix >= end) break;
+      const int pb = pix;
+      advance(pix, x, y);
+      issue(A, pix, x, y);
+      if (pb < end) term(Bs);
+      if (pix >= end) break;
     }
   };
   if (tab && p.rc_taps)
