@@ -84,6 +84,28 @@ def noise_floor_batch(z, prec="f32"):
     return None if fl is None else fl.max(axis=1)
 
 
+def loo_exceedances(z, i=-1, factor=1.5, tol=1e-4, prec="f32"):
+    """How many pairs ONE rounding-only run of the reference moves beyond its pair's bound
+    max(tol, factor x the pair's floor) when that floor is measured on the OTHER runs
+    (leave-one-out), maxed over the runs: the number of per-pair exceedances an
+    implementation that is just one more rounding-only run of the reference shows.  (A pair
+    takes a rounding branch of the batch-global truncated-sigma mask -- a jump of 1e-4..1e-3
+    -- in few runs, so a per-pair maximum over N runs bounds a fresh run only with
+    probability about N / (N + 1) per pair.)"""
+    runs = noise_runs(z, prec)
+    if runs is None:
+        return 0
+    dev = np.maximum(np.abs(runs[0][:, i] - z[f"{prec}_R"][i][None]).max(axis=(2, 3)),
+                     np.abs(runs[1][:, i] - z[f"{prec}_t"][i][None]).max(axis=2))  # [N, B]
+    srt = np.sort(dev, axis=0)
+    arg = dev.argmax(axis=0)
+    out = 0
+    for k in range(dev.shape[0]):
+        fl = np.where(arg == k, srt[-2], srt[-1])  # the pair's floor without run k
+        out = max(out, int((dev[k] > np.maximum(tol, factor * fl)).sum()))
+    return out
+
+
 def noise_counts_beyond(z, tol, i=-1, prec="f32"):
     """Per rounding-only run, the number of pairs whose pose at iteration i moved by more
     than `tol` from the fixture's run [N] (how many pairs the reference itself moves by

@@ -90,18 +90,28 @@ FLOOR_FACTOR = 1.5  # a pair's bound: max(1e-4, 1.5 x its OWN noise floor) (VERD
 def _assert_within_reference_envelope(R, t, z, what="", i=-1):
     """A chained pose (iteration i; R [B,3,3], t [B,3]) against the reference's fp32 and
     fp64 runs, PER PAIR: within 1e-4 or, where the reference's own trajectory of that pair
-    moves by more than that when only rounding changes (golden_io.noise_floor: every update
-    moved by the GPU's one-step deviation, and a one-thread run), within 1.5x that pair's
-    own floor.  Against the fp64 run the pair's bound adds the reference's own fp32-vs-fp64
-    distance of that pair.  Also: no more pairs beyond 1e-4 of the fp32 run than the most
-    any of the reference's own rounding-only runs moves by that much.  Pairs beyond 1e-4 are
-    printed with their floor.  Returns (deviation vs fp32 [B], floor [B])."""
+    moves by more than that when only rounding changes (golden_io.noise_floor: 33 runs, every
+    update moved by the GPU's one-step deviation, and a one-thread run), within 1.5x that
+    pair's own floor.  A per-pair maximum over N runs bounds one more such run only with
+    probability ~N / (N + 1) per pair (a rounding branch of the batch-global truncated-sigma
+    mask is a rare jump), so as many pairs may exceed their bound as ONE of the reference's
+    own runs does against the others' floors (golden_io.loo_exceedances; 0 on most cases) --
+    and those only up to 1.5x the largest rounding-only move of any pair at that iteration.
+    Against the fp64 run each pair's bound is its fp32 bound plus the reference's own
+    fp32-vs-fp64 distance of that pair (the triangle inequality through the fp32 run).  Also:
+    no more pairs beyond 1e-4 of the fp32 run than the most any rounding-only run moves by
+    that much.  Returns (deviation vs fp32 [B], floor [B])."""
     floor = golden_io.noise_floor(z)[i]
     dev = golden_io.pose_deviation(R, t, z, "f32", i)
     bound = np.maximum(SE3_TOL, FLOOR_FACTOR * floor)
-    bad = np.flatnonzero(dev > bound)
-    assert bad.size == 0, (f"{what} iter {i}: pairs beyond max(1e-4, {FLOOR_FACTOR} x own floor): "
-                           + str({int(b): (f"{dev[b]:.2e}", f"floor {floor[b]:.2e}") for b in bad[:20]}))
+    allowed = golden_io.loo_exceedances(z, i, FLOOR_FACTOR, SE3_TOL)
+    over_pair = np.flatnonzero(dev > bound)
+    batch_bound = max(SE3_TOL, FLOOR_FACTOR * float(floor.max()))
+    detail = {int(b): (f"{dev[b]:.2e}", f"floor {floor[b]:.2e}") for b in over_pair[:20]}
+    assert over_pair.size <= allowed, (f"{what} iter {i}: {over_pair.size} pairs beyond max(1e-4, {FLOOR_FACTOR} x own "
+                                       f"floor), the reference's own runs at most {allowed}: {detail}")
+    assert (dev <= batch_bound).all(), f"{what} iter {i}: beyond {FLOOR_FACTOR} x the batch floor: {detail}"
+    bound = np.where(dev > bound, batch_bound, bound)  # the allowed exceedances: the batch bound
     n_over = int((dev > SE3_TOL).sum())
     n_ref = golden_io.noise_counts_beyond(z, SE3_TOL, i)
     assert n_over <= int(n_ref.max()), (f"{what} iter {i}: {n_over} pairs beyond 1e-4 of the fp32 run; the "
@@ -110,22 +120,25 @@ def _assert_within_reference_envelope(R, t, z, what="", i=-1):
         d3264 = np.maximum(np.abs(z["f32_R"][i] - z["f64_R"][i]).max(axis=(1, 2)),
                            np.abs(z["f32_t"][i] - z["f64_t"][i]).max(axis=1))
         dev64 = golden_io.pose_deviation(R, t, z, "f64", i)
-        b64 = np.maximum(SE3_TOL, FLOOR_FACTOR * floor + d3264)
+        b64 = bound + d3264  # the pair's fp32 bound plus the reference's own fp32-to-fp64 distance
         bad = np.flatnonzero(dev64 > b64)
         assert bad.size == 0, (f"{what} iter {i}: vs fp64 beyond the bound: "
                                + str({int(b): (f"{dev64[b]:.2e}", f"bound {b64[b]:.2e}") for b in bad[:20]}))
         over = np.flatnonzero(np.maximum(dev, dev64) > SE3_TOL)
     else:
         over = np.flatnonzero(dev > SE3_TOL)
+    if over_pair.size:
+        print(f"{what} iter {i}: {over_pair.size} pair(s) beyond their own bound (the reference's own runs: up to "
+              f"{allowed}), within {FLOOR_FACTOR} x the batch floor {floor.max():.2e}: {detail}")
     if i in (-1, z["f32_R"].shape[0] - 1):
         print(f"{what}: {dev.size - over.size} of {dev.size} pairs within 1e-4 of both reference runs; max vs fp32 "
               f"{dev.max():.2e}" + (f", vs fp64 {dev64.max():.2e}" if "f64_R" in z else "")
               + f"; batch-max floor {floor.max():.2e} (diagnostic)")
         print(f"  vs the fp32 run alone: {int((dev <= SE3_TOL).sum())} of {dev.size} within 1e-4 ({n_over} beyond; "
-              f"the reference's rounding-only runs: {n_ref.tolist()}), {int((dev <= floor).sum())} within their floor"
-              + (f"; vs the fp64 run: {int((dev64 <= SE3_TOL).sum())} within 1e-4, "
-                 f"{int((dev64 <= d3264 + SE3_TOL).sum())} within the reference's own fp32-fp64 distance + 1e-4"
-                 if "f64_R" in z else ""))
+              f"the reference's rounding-only runs: max {int(n_ref.max())}), {int((dev <= floor).sum())} within "
+              f"their floor" + (f"; vs the fp64 run: {int((dev64 <= SE3_TOL).sum())} within 1e-4, "
+                                 f"{int((dev64 <= d3264 + SE3_TOL).sum())} within the reference's own fp32-fp64 "
+                                 f"distance + 1e-4" if "f64_R" in z else ""))
         if over.size:
             print("  beyond 1e-4 (pair: vs fp32 / vs fp64 / own noise floor / reference fp32-fp64):",
                   {int(b): (f"{dev[b]:.2e}", f"{dev64[b]:.2e}" if "f64_R" in z else "-", f"{floor[b]:.2e}",
@@ -551,7 +564,14 @@ def test_cfg4_sweep_b256():
         # pair in the larger launch); the chained poses then agree within the bound below
         Ra, ta = cb.solve_from_starts(lv, K, Rs[p:p + 1], ts[p:p + 1])
         close = torch.maximum((Rf[p] - Ra[0]).abs().amax((1, 2)), (tf[p] - ta[0]).abs().amax(1)).cpu().numpy()
-        assert (close <= bound).all(), f"start set {p}: grouped vs alone {close.max():.2e}"
+        # two fp32 groupings of the same solve are two rounding samples: each pair within its
+        # bound, but for as many pairs as one of the reference's own runs exceeds against the
+        # others' floors, which stay within 1.5x the batch floor (as _assert_within_reference_envelope)
+        over = np.flatnonzero(close > bound)
+        assert over.size <= golden_io.loo_exceedances(z, -1, FLOOR_FACTOR, SE3_TOL), \
+            f"start set {p}: grouped vs alone, {over.size} pairs beyond their bound (max {close.max():.2e})"
+        assert (close <= max(SE3_TOL, FLOOR_FACTOR * float(floor.max()))).all(), \
+            f"start set {p}: grouped vs alone {close.max():.2e}"
         print(f"start set {p}: grouped vs alone chained poses: {int((close <= 1e-5).sum())} of {B} pairs within "
               f"1e-5, max {close.max():.2e}")
         g0 = (p // G) * G
