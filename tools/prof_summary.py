@@ -32,7 +32,15 @@ def main():
     a = ap.parse_args()
     rows = sorted(csv.DictReader(open(a.trace)), key=lambda r: int(r["Start_Timestamp"]))
     mm_grids = sorted({int(r["Grid_Size_X"]) for r in rows if "minmax" in r["Kernel_Name"]})
-    nrm_grids = sorted({int(r["Grid_Size_X"]) for r in rows if "icp_normals" in r["Kernel_Name"]}, reverse=True)
+    # combine_ICP: the normal-map launch's grid names its level -- the first solve launches
+    # them level 3 .. 0 in order (the grids are distinct per level, but since round 5 they
+    # are not ordered by level size: the kernel's rows per wave adapt to the level)
+    nrm_grids = []
+    for r in sorted(rows, key=lambda r: int(r["Start_Timestamp"])):
+        g = int(r["Grid_Size_X"])
+        if "icp_normals" in r["Kernel_Name"] and g not in nrm_grids:
+            nrm_grids.append(g)
+    nrm_grids.reverse()  # index = level
     top = 3  # coarsest level of the 4-level bench pyramid
     ITERS = 3
     # bench.py --inflight S replays S graphs on S side streams in the timed region; the
