@@ -146,11 +146,15 @@ def batch_create_transform(trs, rot, debug=False):
     """4x4 homogeneous transform(s) from a translation and a rotation (geometry.py:1139-1149):
     numpy [3] + [3,3] -> [4,4]; torch [B,3] + [B,3,3] -> [B,4,4] on rot's device.  `debug` is
     accepted for signature parity and ignored, as there; the bottom row moves device only
-    (its float32 zeros / ones promote with `top` in the concatenation, as there)."""
+    (its float32 zeros / ones promote with `top` in the concatenation, as there).  A torch
+    translation of [B,3,1] -- what LeastSquareTracking.forward returns, and what kf_vo.py:173
+    passes -- is taken as [B,3] (the reference's concatenation raises on it)."""
     if isinstance(trs, np.ndarray):
         top = np.hstack((rot, trs.reshape(3, 1)))
         return np.vstack((top, np.hstack((np.zeros([1, 3]), np.ones([1, 1])))))
     B = trs.shape[0]
+    if trs.dim() == 3:
+        trs = trs.reshape(B, 3)
     top = torch.cat((rot, trs.unsqueeze(2)), dim=2)
     bot = torch.cat((torch.zeros(B, 1, 3), torch.ones(B, 1, 1)), 2).to(top.device)
     return torch.cat((top, bot), dim=1)

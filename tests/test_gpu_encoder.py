@@ -146,7 +146,8 @@ def test_dropin_encoder_writes_packed_features():
     relayout pass in the forward): the packed features are bit for bit the heads' conv
     outputs through the in-place epilogue and the relayout (captured by hooks on the heads'
     convolutions -- MIOpen's convolution algorithms are not bitwise reproducible from one
-    call to the next, so two forwards are not compared), and the forward solves on them."""
+    call to the next, so two forwards are not compared), and the forward solves on them: the same
+    prepared features give the same poses twice, and within 1e-5 of the NCHW path's."""
     from deep_prob_feature_track_amd import ic
     from deep_prob_feature_track_amd.examples import K_FULL, color_float, depth_m, load_synthetic_weights
     from deep_prob_feature_track_amd.models.LeastSquareTracking import LeastSquareTracking, default_options
@@ -179,3 +180,18 @@ def test_dropin_encoder_writes_packed_features():
             assert ic.bn_elu_(y, getattr(net.encoder, f"f_conv{l}")[1])
             assert torch.equal(x, ic.pack_features(y)), f"level {l} frame {f}"
     assert torch.isfinite(R).all() and torch.isfinite(t).all()
+    # the poses: forward on the prepared (packed) features is deterministic, and equals the
+    # forward on the same features unpacked to NCHW (the NCHW tile path) within 1e-5
+    prep = tuple(prep)
+    unpacked = list(prep)
+    for i in (2, 3):
+        unpacked[i] = [ic.unpack_features(x) for x in prep[i]]
+    poses = []
+    with torch.no_grad():
+        for P in (prep, prep, tuple(unpacked)):
+            net._preprocess = lambda *a, _P=P, **k: _P
+            poses.append(net(img0, img1, d0, d1, K))
+    del net._preprocess
+    assert torch.equal(poses[0][0], poses[1][0]) and torch.equal(poses[0][1], poses[1][1])
+    assert (poses[0][0] - poses[2][0]).abs().max().item() < 1e-5
+    assert (poses[0][1] - poses[2][1]).abs().max().item() < 1e-5

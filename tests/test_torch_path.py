@@ -8,7 +8,9 @@ CPU tensors and calls with gradients, pinned against the reference's own outputs
   solve ends within each pair's bound (max(1e-4, 1.5x its own noise floor)).
 * Module level: the drop-in `LeastSquareTracking` on CPU against the reference module's
   outputs (tests/golden/gen_model_golden.py), for every configuration, and the reference's
-  `run_example.py` call sequence (run_example.py:84-105) replayed through the `models` alias.
+  `run_example.py` call sequence (run_example.py:84-105) and kf_vo.py's per-frame forward
+  (kf_vo.py:155-175) replayed through the `models` alias, on the CPU and (marked gpu) with the
+  GPU visible.
 * Gradients: the solve is differentiable (finite gradients into the features) and equals the
   no-grad result; training-mode forward returns the stacked per-level poses
   (LeastSquareTracking.py:568-575) with gradients into the encoder.
@@ -131,8 +133,11 @@ import numpy as np
 import torch
 sys.path[:0] = [os.path.join(sys.argv[1], "tests"), os.path.join(sys.argv[1], "tests", "golden")]
 import models.LeastSquareTracking as ICtracking          # run_example.py:16, through the alias
+from models.geometry import batch_create_transform       # kf_vo.py:17, through the alias
+from train_utils_replay import check_cuda
 import recipe, gen_model_golden as G
-case, enc, unc, mest, solver, kw = sys.argv[2], sys.argv[3], sys.argv[4], sys.argv[5], sys.argv[6], eval(sys.argv[7])
+mode, case, enc, unc, mest, solver, kw = sys.argv[2:9]
+kw = eval(kw)
 net = ICtracking.LeastSquareTracking(encoder_name=enc, max_iter_per_pyr=3, mEst_type=mest, solver_type=solver,
                                      uncertainty_type=unc, direction='inverse', **kw)   # run_example.py:84-92
 if torch.cuda.is_available():                                                          # run_example.py:102-103
@@ -143,36 +148,97 @@ net.load_state_dict({k: torch.from_numpy(recipe.synthetic_weights(k, v.shape)) f
 net.eval()                                                                             # run_example.py:44
 spec = G.MODEL_CASES[case]
 batch = [torch.from_numpy(v) for k, v in G.model_inputs(spec["pairs"], False).items()]
-color0, color1, depth0, depth1, K = batch   # check_cuda (train_utils.py:13-26): no GPU, stays on the host
-with torch.no_grad():                                                                  # run_example.py:55-56
-    R, t = net.forward(color0, color1, depth0, depth1, K)
+color0, color1, depth0, depth1, K = check_cuda(batch)                                  # run_example.py:54
 z = np.load(os.path.join(sys.argv[1], "tests", "golden", f"model_{case}.npz"))
-print("DEV", float(np.abs(R.numpy() - z["R"]).max()), float(np.abs(t.numpy().reshape(-1, 3) - z["t"].reshape(-1, 3)).max()))
+if mode == "run_example":
+    with torch.no_grad():                                                              # run_example.py:55-56
+        R, t = net.forward(color0, color1, depth0, depth1, K)
+    R, t = R.cpu().numpy(), t.cpu().numpy().reshape(-1, 3)
+else:  # kf_vo.py:155-175: one frame pair per forward (B = 1), poses as 4x4 transforms
+    Rs, ts = [], []
+    for i in range(color0.shape[0]):
+        with torch.no_grad():
+            c0, c1 = color0[i].unsqueeze(dim=0), color1[i].unsqueeze(dim=0)
+            d0, d1 = depth0[i].unsqueeze(dim=0), depth1[i].unsqueeze(dim=0)
+            intrins = K[i].unsqueeze(dim=0)
+            output = net.forward(c0, c1, d0, d1, intrins)
+        R, t = output
+        T_CR = batch_create_transform(t, R).squeeze(dim=0).cpu().numpy()
+        Rs.append(T_CR[:3, :3])
+        ts.append(T_CR[:3, 3])
+    R, t = np.stack(Rs), np.stack(ts)
+print("DEV", float(np.abs(R - z["R"]).max()), float(np.abs(t - z["t"].reshape(-1, 3)).max()))
 """
 
+# train_utils.check_cuda (train_utils.py:13-26), restated for the replay: tensors to the GPU
+# when there is one, else unchanged
+_CHECK_CUDA = """import torch
 
-@pytest.mark.parametrize("case,enc,unc,mest,solver,kw", [
-    # run_example.py's own constructor (ConvRGBD2, MultiScale2w, Direct-ResVol, the IC tracker;
-    # its options are the drop-in's config defaults = the fixture's select_deepic configuration)
-    ("select_deepic", "ConvRGBD2", "None", "MultiScale2w", "Direct-ResVol", "{}"),
-    # the U_IC configuration of the shipped eval scripts (laplacian uncertainty, 8 channels)
-    ("convrgbd2_c8", "ConvRGBD2", "laplacian", "None", "Direct-Nodamping",
-     "dict(feature_channel=8, uncertainty_channel=1, feature_extract='conv', remove_tru_sigma=True)"),
-])
-def test_run_example_call_sequence_replays_on_cpu(tmp_path, case, enc, unc, mest, solver, kw):
-    """run_example.py's calls (construct -> .cuda() when a GPU is there -> load_state_dict ->
-    eval -> forward under no_grad) in a child interpreter with only PYTHONPATH changed
-    (dropin/sitecustomize.py) and a shadowing `models/` package in its directory, on a host
-    without a visible GPU: the poses land within 1e-4 of the reference module's."""
+
+def check_cuda(items):
+    if not torch.cuda.is_available():
+        return items
+    return [x.cuda() if torch.is_tensor(x) else x for x in items]
+"""
+
+# run_example.py's own constructor (ConvRGBD2, MultiScale2w, Direct-ResVol, the IC tracker;
+# its options are the drop-in's config defaults = the fixture's select_deepic configuration),
+# and the U_IC configuration of the shipped eval scripts (laplacian uncertainty, 8 channels)
+_CONFIGS = {
+    "select_deepic": ("ConvRGBD2", "None", "MultiScale2w", "Direct-ResVol", "{}"),
+    "convrgbd2_c8": ("ConvRGBD2", "laplacian", "None", "Direct-Nodamping",
+                     "dict(feature_channel=8, uncertainty_channel=1, feature_extract='conv', remove_tru_sigma=True)"),
+    # the IC tracker with the learned M-estimator on raw intensity, one pair (kf_vo.py's B = 1)
+    "rgb_ic_mest2w": ("RGB", "None", "MultiScale2w", "Direct-Nodamping",
+                      "dict(feature_channel=1, uncertainty_channel=1, feature_extract='average', remove_tru_sigma=False, "
+                      "combine_ICP=False, scaler='None', init_pose_type='identity')"),
+}
+
+
+def replay(tmp_path, mode, case, gpu=False):
+    """Run a caller's call sequence (`mode`: run_example.py:84-105, or kf_vo.py:155-175's
+    per-frame B = 1 forwards) in a child interpreter with only PYTHONPATH changed
+    (dropin/sitecustomize.py) and a shadowing `models/` package in its directory; the GPU
+    hidden unless `gpu`.  Returns the largest |dR|, |dt| against the reference module's poses."""
     shadow = tmp_path / "models"
     shadow.mkdir()
     (shadow / "__init__.py").write_text("raise ImportError('the shadowed package was imported')\n")
-    env = dict(os.environ, PYTHONPATH=os.path.join(ROOT, "dropin"), PYTHONDONTWRITEBYTECODE="1",
-               HIP_VISIBLE_DEVICES="", CUDA_VISIBLE_DEVICES="")
-    r = subprocess.run([sys.executable, "-c", _REPLAY, ROOT, case, enc, unc, mest, solver, kw], cwd=tmp_path, env=env,
+    (tmp_path / "train_utils_replay.py").write_text(_CHECK_CUDA)
+    env = dict(os.environ, PYTHONPATH=os.pathsep.join([os.path.join(ROOT, "dropin"), str(tmp_path)]),
+               PYTHONDONTWRITEBYTECODE="1")
+    if not gpu:
+        env.update(HIP_VISIBLE_DEVICES="", CUDA_VISIBLE_DEVICES="")
+    r = subprocess.run([sys.executable, "-c", _REPLAY, ROOT, mode, case, *_CONFIGS[case]], cwd=tmp_path, env=env,
                        capture_output=True, text=True, timeout=600)
     assert r.returncode == 0, r.stderr[-3000:]
-    dR, dt = (float(x) for x in r.stdout.strip().splitlines()[-1].split()[1:])
+    return tuple(float(x) for x in r.stdout.strip().splitlines()[-1].split()[1:])
+
+
+@pytest.mark.parametrize("case", ["select_deepic", "convrgbd2_c8"])
+def test_run_example_call_sequence_replays_on_cpu(tmp_path, case):
+    """run_example.py's calls (construct -> .cuda() when a GPU is there -> load_state_dict ->
+    eval -> check_cuda -> forward under no_grad) on a host without a visible GPU: the poses
+    land within 1e-4 of the reference module's."""
+    dR, dt = replay(tmp_path, "run_example", case)
+    assert dR < 1e-4 and dt < 1e-4, (dR, dt)
+
+
+def test_kf_vo_call_sequence_replays_on_cpu(tmp_path):
+    """kf_vo.py's per-frame calls (a B = 1 forward, its pose through batch_create_transform)
+    on a one-pair fixture (a pair solved alone is not the pair solved in a batch: the
+    pyramid's batch-global extrema): within 1e-4 of the reference module's pose."""
+    dR, dt = replay(tmp_path, "kf_vo", "rgb_ic_mest2w")
+    assert dR < 1e-4 and dt < 1e-4, (dR, dt)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("mode,case", [("run_example", "select_deepic"), ("run_example", "convrgbd2_c8"),
+                                       ("kf_vo", "rgb_ic_mest2w")])
+def test_caller_call_sequences_replay_on_the_gpu(tmp_path, mode, case):
+    """The same replays with the GPU visible: net.cuda(), check_cuda moves the batch, forward
+    runs the HIP library (the encoder on MIOpen): within 1e-4 of the reference module's poses
+    (computed on the CPU)."""
+    dR, dt = replay(tmp_path, mode, case, gpu=True)
     assert dR < 1e-4 and dt < 1e-4, (dR, dt)
 
 
