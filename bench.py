@@ -119,13 +119,15 @@ def l0_traffic(pairs, group, kernel, icp=False):
     build.py records beside the library) and on the same launch shape."""
     import glob
     from deep_prob_feature_track_amd import build as Bd
-    isa = json.load(open(Bd.ISA_OUT)).get(kernel) if os.path.exists(Bd.ISA_OUT) else None
-    if isa is None:
+    hashes = json.load(open(Bd.ISA_OUT)) if os.path.exists(Bd.ISA_OUT) else {}
+    isa = hashes.get(kernel)
+    isa_icp = hashes.get(Bd.ICP_KERNEL) if icp else None  # the cfg5 iteration: the ICP pass too
+    if isa is None or (icp and isa_icp is None):
         return None
     for f in sorted(glob.glob(os.path.join(ROOT, "profiles", "*_l0_traffic.json")), reverse=True):
         d = json.load(open(f))
         if (d.get("pairs_per_launch", 8) == pairs and d.get("group", pairs) == group and d.get("isa_sha256") == isa
-                and bool(d.get("combine_icp", False)) == icp):
+                and bool(d.get("combine_icp", False)) == icp and d.get("isa_sha256_icp") == isa_icp):
             return {"hbm_bytes": d["hbm_bytes"], "source": os.path.relpath(f, ROOT)}
     return None
 

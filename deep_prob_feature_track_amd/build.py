@@ -63,6 +63,8 @@ LLVM_BIN = "/opt/rocm/lib/llvm/bin"
 ISA_OUT = os.path.join(HERE, "libdpft_ic.isa.json")
 # the level-0/1 marching kernel of the bench (C = 32, one sigma plane, remove_tru_sigma, U_IC, channel quads)
 L0_KERNEL = "_ZN12_GLOBAL__N_116ic_reduce_kernelILi32ELb1ELb1ELi0ELb1EEEvNS_10IterParamsE"
+# the combine_ICP pass that runs in front of it in a cfg5 (bench.py --icp) iteration
+ICP_KERNEL = "_ZN12_GLOBAL__N_118icp_records_kernelENS_10IterParamsEPf"
 
 
 def isa_hashes(so_path=OUT):

@@ -872,10 +872,14 @@ __global__ __launch_bounds__(kThreads) void icp_records_kernel(IterParams p, flo
       float d0;
       bool m0;
     };
-    auto issue = [&](Stage& S, int pix, int x, int y) {
+    // depth0 one pixel further ahead (`dq`): loaded when the pixel before it is issued, so
+    // the geometry and the tap loads of an issue wait on no load (the pass is bound by this
+    // dependent chain, not by its VALU: level-0 iteration 2285 -> 2255 us, +0.9 % for cfg5)
+    auto ld0 = [&](int pix) { return d0b[min(pix, end - 1)]; };
+    auto issue = [&](Stage& S, int pix, int x, int y, float d0) {
       const int pc = min(pix, end - 1);
       S.m0 = m0b ? (m0b[pc] != 0) : true;
-      S.d0 = d0b[pc];
+      S.d0 = d0;
       S.g = icp_geo(ncx(x), ncy(min(y, H - 1)), S.d0, Rm, tv, fx, fy, cx, cy, H, W, RC ? rsxy : nullptr);
       S.q = icp_load(S.g, nd1);
     };
@@ -901,16 +905,20 @@ __global__ __launch_bounds__(kThreads) void icp_records_kernel(IterParams p, flo
     };
     int pix = beg + tid, y = pix / W, x = pix - y * W;  // then advanced by kThreads without a division
     Stage A, Bs;
-    issue(A, pix, x, y);
+    float dq = ld0(pix);
+    issue(A, pix, x, y, dq);
+    dq = ld0(pix + kThreads);
     for (;;) {
       const int pa = pix;
       advance(pix, x, y);
-      issue(Bs, pix, x, y);
+      issue(Bs, pix, x, y, dq);
+      dq = ld0(pix + kThreads);
       if (pa < end) term(A);
       if (pix >= end) break;
       const int pb = pix;
       advance(pix, x, y);
-      issue(A, pix, x, y);
+      issue(A, pix, x, y, dq);
+      dq = ld0(pix + kThreads);
       if (pb < end) term(Bs);
       if (pix >= end) break;
     }

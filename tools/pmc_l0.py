@@ -93,7 +93,8 @@ def main():
     out = {"kernel": f"ic_reduce_kernel<32,Cs=1,tru,U_IC,c4>{' + icp_records_kernel' if a.icp else ''} level 0, {a.groups} x 8 pairs per launch, 640x480 "
                      "(tools/kbench.py --mode level --from-solve)",
            "pairs_per_launch": 8 * a.groups, "group": 8,
-           "src_sha256": src_sha(), "isa_sha256": isa_sha(kernel), "combine_icp": a.icp, "launches": {"fetch": nf, "write": nw},
+           "src_sha256": src_sha(), "isa_sha256": isa_sha(kernel), "combine_icp": a.icp,
+           **({"isa_sha256_icp": isa_sha(B.ICP_KERNEL)} if a.icp else {}), "launches": {"fetch": nf, "write": nw},
            "FETCH_SIZE_KiB": fetch, "WRITE_SIZE_KiB": write,
            "read_bytes": 2 * 1024 * fetch, "write_bytes": 1024 * write,
            "hbm_bytes": 2 * 1024 * fetch + 1024 * write,
