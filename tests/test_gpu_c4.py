@@ -262,11 +262,15 @@ def test_c4_schedules_random(schedule, C, H, W, no_unc, masks):
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("reverse", [False, True])
-@pytest.mark.parametrize("C,H,W,masks", [(32, 45, 131, True), (16, 64, 70, False), (32, 120, 160, False)])
+@pytest.mark.parametrize("C,H,W,masks", [(32, 45, 131, True), (16, 64, 70, False), (32, 120, 160, False),
+                                         (16, 6, 2050, False)])
 def test_c4_combine_icp_march(C, H, W, masks, reverse):
     """combine_ICP (MODE 1) on the channel-quad marching path (C = 16 / 32: the ring, the
     tap cache and the per-pixel ICP term of ic_reduce_kernel<..., true>), forward and
-    reverse marching order, against the NCHW kernel on the same inputs."""
+    reverse marching order, against the NCHW kernel on the same inputs.  The sizes reach every
+    pixel loop of the ICP records pass: masks; no masks with the coordinate table and IEEE tap
+    divisions (64 x 70: not a verified divisor size); with the constant-divisor taps (120 x 160);
+    without the table (W + H > kIcpTab, 6 x 2050)."""
     from deep_prob_feature_track_amd import ic
     dev = _dev()
     g = torch.Generator().manual_seed(C * 7 + H)
