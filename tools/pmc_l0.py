@@ -40,9 +40,9 @@ def isa_sha(kernel=None):
     return (B.isa_hashes(os.path.abspath(lib)) if lib else json.load(open(B.ISA_OUT))).get(kernel or B.L0_KERNEL)
 
 
-def run_pass(counter, outdir, groups, icp=False):
+def run_pass(counter, outdir, groups, icp=False, level=0):
     cmd = ["timeout", "-s", "KILL", "90", "rocprofv3", "--pmc", counter, "--output-format", "csv", "-d", outdir,
-           "-o", "c", "--", sys.executable, os.path.join(ROOT, "tools", "kbench.py"), "--c4", "--level", "0",
+           "-o", "c", "--", sys.executable, os.path.join(ROOT, "tools", "kbench.py"), "--c4", "--level", str(level),
            "--mode", "level", "--from-solve", "--reps", "10", "--warm-ms", "0", "--groups", str(groups)] + (["--icp"] if icp else [])
     env = dict(os.environ, TMPDIR="/tmp")
     if env.get("DPFT_LIB"):  # a variant library (tools/build_variants.py); the profiler runs from /tmp
@@ -78,6 +78,8 @@ def main():
     ap.add_argument("--out", required=True)
     ap.add_argument("--groups", type=int, default=16, help="8-pair batches per launch (bench.py --groups)")
     ap.add_argument("--icp", action="store_true", help="the combine_ICP kernel (bench.py --icp)")
+    ap.add_argument("--level", type=int, default=0, help="pyramid level of the measured launches (traffic "
+                    "of the coarser levels; only level 0 is matched by bench.py)")
     ap.add_argument("--from-dir", help="parse the fetch/ and write/ CSVs under this directory instead of running")
     a = ap.parse_args()
     tmp = os.path.join(ROOT, "gpurun_out", "pmc_l0")
@@ -85,14 +87,14 @@ def main():
         fetch, nf = parse("FETCH_SIZE", os.path.join(a.from_dir, "fetch"))
         write, nw = parse("WRITE_SIZE", os.path.join(a.from_dir, "write"))
     else:
-        fetch, nf = run_pass("FETCH_SIZE", os.path.join(tmp, "fetch"), a.groups, a.icp)
-        write, nw = run_pass("WRITE_SIZE", os.path.join(tmp, "write"), a.groups, a.icp)
+        fetch, nf = run_pass("FETCH_SIZE", os.path.join(tmp, "fetch"), a.groups, a.icp, a.level)
+        write, nw = run_pass("WRITE_SIZE", os.path.join(tmp, "write"), a.groups, a.icp, a.level)
     sys.path.insert(0, ROOT)
     from deep_prob_feature_track_amd import build as B
     kernel = B.L0_KERNEL
-    out = {"kernel": f"ic_reduce_kernel<32,Cs=1,tru,U_IC,c4>{' + icp_records_kernel' if a.icp else ''} level 0, {a.groups} x 8 pairs per launch, 640x480 "
+    out = {"kernel": f"ic_reduce_kernel<32,Cs=1,tru,U_IC,c4>{' + icp_records_kernel' if a.icp else ''} level {a.level}, {a.groups} x 8 pairs per launch, 640x480 "
                      "(tools/kbench.py --mode level --from-solve)",
-           "pairs_per_launch": 8 * a.groups, "group": 8,
+           "level": a.level, "pairs_per_launch": 8 * a.groups, "group": 8,
            "src_sha256": src_sha(), "isa_sha256": isa_sha(kernel), "combine_icp": a.icp,
            **({"isa_sha256_icp": isa_sha(B.ICP_KERNEL)} if a.icp else {}), "launches": {"fetch": nf, "write": nw},
            "FETCH_SIZE_KiB": fetch, "WRITE_SIZE_KiB": write,
