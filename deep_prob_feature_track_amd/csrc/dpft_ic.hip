@@ -2854,6 +2854,36 @@ __global__ __launch_bounds__(kThreads) void pack_c4_kernel(const float* __restri
   dst[i] = f32x4{s[0], s[HW], s[2 * (long)HW], s[3 * (long)HW]};
 }
 
+// The same for a solve entered with NCHW features (pack_on_entry): f0 and f1 in one launch
+// (blockIdx.y), four pixels per thread -- one 16-byte load from each of the quad's four
+// planes, a 4 x 4 register transpose, four 16-byte stores (64 contiguous bytes per lane).
+__global__ __launch_bounds__(kThreads) void pack_c4_x4_kernel(const float* __restrict__ a, const float* __restrict__ b,
+                                                              f32x4* __restrict__ da, f32x4* __restrict__ db, long n,
+                                                              long HW4) {
+  const long i = (long)blockIdx.x * kThreads + threadIdx.x;  // (b * C/4 + q) * HW / 4 + pixel group
+  if (i >= n) return;
+  const f32x4* s = reinterpret_cast<const f32x4*>(blockIdx.y ? b : a);
+  f32x4* o = (blockIdx.y ? db : da) + 4 * i;
+  const long bq = i / HW4, g = i - bq * HW4;
+  const f32x4* sp = s + bq * 4 * HW4 + g;
+  const f32x4 c0 = __builtin_nontemporal_load(sp), c1 = __builtin_nontemporal_load(sp + HW4),
+              c2 = __builtin_nontemporal_load(sp + 2 * HW4), c3 = __builtin_nontemporal_load(sp + 3 * HW4);
+  o[0] = f32x4{c0.x, c1.x, c2.x, c3.x};
+  o[1] = f32x4{c0.y, c1.y, c2.y, c3.y};
+  o[2] = f32x4{c0.z, c1.z, c2.z, c3.z};
+  o[3] = f32x4{c0.w, c1.w, c2.w, c3.w};
+}
+// (any H W or alignment: one pixel per thread, as pack_c4_kernel, f0 / f1 by blockIdx.y)
+__global__ __launch_bounds__(kThreads) void pack_c4_pair_kernel(const float* __restrict__ a, const float* __restrict__ b,
+                                                                f32x4* __restrict__ da, f32x4* __restrict__ db, long n,
+                                                                long HW) {
+  const long i = (long)blockIdx.x * kThreads + threadIdx.x;
+  if (i >= n) return;
+  const long bq = i / HW, pix = i - bq * HW;
+  const float* s = (blockIdx.y ? b : a) + bq * 4 * HW + pix;
+  (blockIdx.y ? db : da)[i] = f32x4{s[0], s[HW], s[2 * HW], s[3 * HW]};
+}
+
 // NHWC (channels_last) -> channel-quad layout: thread r of pair row b = blockIdx.y reads
 // the 16-byte quad r of the pair's [HW][C] block (a linear, coalesced read) and writes it
 // to plane q = r % Q at pixel r / Q (64 lanes = 64 / Q pixels x Q planes: one 128-byte run
@@ -3140,9 +3170,24 @@ size_t icp_rec_offset(const DpftLevelDesc& d) {
   return kCtrlBytes + prec_bytes(d) + (((size_t)d.B * 4 * d.H * d.W * sizeof(float) + 255) & ~(size_t)255);
 }
 
-size_t ws_need(const DpftLevelDesc& d) {
+// every entry point's own regions: control words, pair / ICP / workgroup records
+size_t ws_core(const DpftLevelDesc& d) {
   return kCtrlBytes + prec_bytes(d) + ((nrm_bytes(d) + 255) & ~(size_t)255) + rec_bytes(d);
 }
+// NCHW features handed to a solve (the reference's layout, algorithms.py:611-723) are packed
+// once on entry into the workspace's channel-quad copy, and the level's iterations run the
+// channel-quad kernels on it: where those are the marching / split kernels (C % 16 == 0) and
+// the level has one sigma plane (or none), from two iterations on.  The NCHW kernel (the tile
+// path) reads f1's taps channel plane by channel plane at half the rate.
+bool packs_on_entry(const DpftLevelDesc& d) {
+  return !(d.flags & DPFT_FEATURES_C4) && d.C % 16 == 0 && (d.Cs == 1 || (d.flags & DPFT_NO_UNCERTAINTY)) &&
+         d.iters >= 2;
+}
+size_t pack_plane_bytes(const DpftLevelDesc& d) {
+  return ((size_t)d.B * d.C * d.H * d.W * sizeof(float) + 255) & ~(size_t)255;
+}
+// + the packed f0 / f1 of a solve entered with NCHW features (packs_on_entry)
+size_t ws_need(const DpftLevelDesc& d) { return ws_core(d) + (packs_on_entry(d) ? 2 * pack_plane_bytes(d) : 0); }
 size_t nrm_offset(const DpftLevelDesc& d) { return kCtrlBytes + prec_bytes(d); }
 size_t rec_offset(const DpftLevelDesc& d) { return kCtrlBytes + prec_bytes(d) + ((nrm_bytes(d) + 255) & ~(size_t)255); }
 
@@ -3435,7 +3480,7 @@ int iterate_impl(const DpftLevelDesc* desc, const DpftLevelTensors* tt, float* R
   if (rc) return rc;
   if ((rc = check_tensors(tt, desc->flags))) return rc;
   if (!R || !t || !ws) return fail(DPFT_E_INVALID, "null pose / workspace");
-  if (ws_bytes < ws_need(*desc)) return fail(DPFT_E_WORKSPACE, "workspace %zu < %zu", ws_bytes, ws_need(*desc));
+  if (ws_bytes < ws_core(*desc)) return fail(DPFT_E_WORKSPACE, "workspace %zu < %zu", ws_bytes, ws_core(*desc));
   const Geometry g = plan(*desc);
   if ((first & DPFT_ITER_FIRST) && (rc = launch_minmax(*desc, *tt, ws, st))) return rc;
   IterParams p = make_params(*desc, *tt, g, R, t, ws);
@@ -3450,10 +3495,38 @@ int iterate_impl(const DpftLevelDesc* desc, const DpftLevelTensors* tt, float* R
   return launch_reduce(p, st);
 }
 
-int solve_level_impl(const DpftLevelDesc* desc, const DpftLevelTensors* tensors, float* R, float* t, float* jtj_out,
-                     float* jtr_out, void* ws, size_t ws_bytes, hipStream_t st) {
-  int rc = check_desc(desc);
+// f0 and f1 [B,C,H,W] -> channel-quad copies in the workspace (packs_on_entry), one launch
+int pack_on_entry(const DpftLevelDesc& d, DpftLevelDesc& dc, DpftLevelTensors& tc, void* ws, size_t ws_bytes,
+                  hipStream_t st) {
+  if (ws_bytes < ws_need(d)) return fail(DPFT_E_WORKSPACE, "workspace %zu < %zu", ws_bytes, ws_need(d));
+  if (!tc.f0 || !tc.f1) return fail(DPFT_E_INVALID, "null tensor pointer");
+  f32x4* p0 = reinterpret_cast<f32x4*>(static_cast<char*>(ws) + ws_core(d));
+  f32x4* p1 = reinterpret_cast<f32x4*>(static_cast<char*>(ws) + ws_core(d) + pack_plane_bytes(d));
+  const long HW = (long)d.H * d.W, quads = (long)d.B * (d.C / 4);
+  const bool x4 = HW % 4 == 0 && ((uintptr_t)tc.f0 % 16) == 0 && ((uintptr_t)tc.f1 % 16) == 0;
+  const long n = x4 ? quads * (HW / 4) : quads * HW;
+  const dim3 grid((unsigned)((n + kThreads - 1) / kThreads), 2);
+  if (x4)
+    hipLaunchKernelGGL(pack_c4_x4_kernel, grid, dim3(kThreads), 0, st, tc.f0, tc.f1, p0, p1, n, HW / 4);
+  else
+    hipLaunchKernelGGL(pack_c4_pair_kernel, grid, dim3(kThreads), 0, st, tc.f0, tc.f1, p0, p1, n, HW);
+  int rc = hip_check("pack_c4 (solve entry)");
   if (rc) return rc;
+  tc.f0 = reinterpret_cast<const float*>(p0);
+  tc.f1 = reinterpret_cast<const float*>(p1);
+  dc.flags |= DPFT_FEATURES_C4;
+  return DPFT_OK;
+}
+
+int solve_level_impl(const DpftLevelDesc* desc_in, const DpftLevelTensors* tensors_in, float* R, float* t,
+                     float* jtj_out, float* jtr_out, void* ws, size_t ws_bytes, hipStream_t st) {
+  int rc = check_desc(desc_in);
+  if (rc) return rc;
+  DpftLevelDesc dc = *desc_in;
+  DpftLevelTensors tc = tensors_in ? *tensors_in : DpftLevelTensors{};
+  if (tensors_in && packs_on_entry(dc) && (rc = pack_on_entry(*desc_in, dc, tc, ws, ws_bytes, st))) return rc;
+  const DpftLevelDesc* desc = &dc;
+  const DpftLevelTensors* tensors = tensors_in ? &tc : nullptr;
   for (int it = 0; it < desc->iters; ++it) {
     const bool last = it == desc->iters - 1;
     const int flags = (it == 0 ? DPFT_ITER_FIRST : 0) | ((it & 1) ? DPFT_ITER_REVERSE : 0);
@@ -3575,7 +3648,7 @@ int dpft_ic_reduce_only(const DpftLevelDesc* desc, const DpftLevelTensors* tt, c
   int rc = check_desc(desc);
   if (rc) return rc;
   if ((rc = check_tensors(tt, desc->flags))) return rc;
-  if (ws_bytes < ws_need(*desc)) return fail(DPFT_E_WORKSPACE, "workspace %zu < %zu", ws_bytes, ws_need(*desc));
+  if (ws_bytes < ws_core(*desc)) return fail(DPFT_E_WORKSPACE, "workspace %zu < %zu", ws_bytes, ws_core(*desc));
   const Geometry g = plan(*desc);
   return launch_reduce(make_params(*desc, *tt, g, R, t, ws), static_cast<hipStream_t>(hip_stream));
 }
@@ -3585,7 +3658,7 @@ int dpft_ic_debug_pixels(const DpftLevelDesc* desc, const DpftLevelTensors* tt, 
   int rc = check_desc(desc);
   if (rc) return rc;
   if ((rc = check_tensors(tt, desc->flags))) return rc;
-  if (!out || ws_bytes < ws_need(*desc)) return fail(DPFT_E_INVALID, "null output or small workspace");
+  if (!out || ws_bytes < ws_core(*desc)) return fail(DPFT_E_INVALID, "null output or small workspace");
   const Geometry g = plan(*desc);
   const IterParams p = make_params(*desc, *tt, g, R, t, ws);
   const int n = desc->B * desc->H * desc->W;
@@ -3601,7 +3674,7 @@ int dpft_ic_residual_map(const DpftLevelDesc* desc, const DpftLevelTensors* tt, 
   if ((rc = check_tensors(tt, desc->flags))) return rc;
   if (!(desc->flags & DPFT_NO_UNCERTAINTY))
     return fail(DPFT_E_INVALID, "the residual map is the IC tracker's (DPFT_NO_UNCERTAINTY)");
-  if (!R || !t || !out || !ws || ws_bytes < ws_need(*desc)) return fail(DPFT_E_INVALID, "null pointer or small workspace");
+  if (!R || !t || !out || !ws || ws_bytes < ws_core(*desc)) return fail(DPFT_E_INVALID, "null pointer or small workspace");
   const Geometry g = plan(*desc);
   const IterParams p = make_params(*desc, *tt, g, R, t, ws);
   const long n = (long)desc->B * desc->H * desc->W;
@@ -3636,7 +3709,7 @@ int sigma_extrema_impl(const DpftLevelDesc* descs, const DpftLevelTensors* tenso
     const int xslot = (int)((d.flags & DPFT_EXT_SLOT_MASK) >> DPFT_EXT_SLOT_SHIFT);
     if (!xslot) return fail(DPFT_E_INVALID, "level %d has no extrema slot (DPFT_EXT_SLOT)", l);
     if (!tensors[l].s0) return fail(DPFT_E_INVALID, "level %d: null sigma0", l);
-    if (workspace_bytes < ws_need(d)) return fail(DPFT_E_WORKSPACE, "workspace %zu < %zu", workspace_bytes, ws_need(d));
+    if (workspace_bytes < ws_core(d)) return fail(DPFT_E_WORKSPACE, "workspace %zu < %zu", workspace_bytes, ws_core(d));
     if (l == 0) a.groups = d.B / group_of(d);
     if (d.B / group_of(d) != a.groups) return fail(DPFT_E_INVALID, "level %d: another DPFT_GROUP than level 0", l);
     a.s[l] = tensors[l].s0;

@@ -151,9 +151,10 @@ class LeastSquareTracking(nn.Module):
     # ------------------------------------------------------------------ API
     def forward(self, img0, img1, depth0, depth1, K, init_only=False, logger=None, iteration=0, vis=False,
                 obj_mask0=None, obj_mask1=None, index=None):
-        """Coarse-to-fine tracking (LeastSquareTracking.py:311-577); returns [R, t], or in
-        training mode the per-level poses stacked, (R [B,L,3,3], t [B,L,3,1][, JtWJ [B,L,6,6]])
-        with L = 4 (5 with a trained init pose, its pose first), levels 3 .. 0."""
+        """Coarse-to-fine tracking (LeastSquareTracking.py:311-577); returns [R [B,3,3], t [B,3]]
+        (t as the reference's batch_Rt_compose leaves it, geometry.py:122), or in training mode
+        the per-level poses stacked, (R [B,L,3,3], t [B,L,3][, JtWJ [B,L,6,6]]) with L = 4 (5 with
+        a trained init pose, its pose first), levels 3 .. 0."""
         (I0, I1, x0, x1, sigma0, sigma1, dpt0, dpt1, inv_d0, inv_d1, m0, m1, poseI) = self._preprocess(
             img0, img1, depth0, depth1, poseI=None, obj_mask0=obj_mask0, obj_mask1=obj_mask1)
         if self.training:
@@ -208,9 +209,10 @@ class LeastSquareTracking(nn.Module):
         """Training-mode forward (LeastSquareTracking.py:333-445, 568-575) on the PyTorch path:
         every level's pose (and JtWJ with uncer_prop) collected, gradients kept."""
         poses, sig = [[], []], []
+        B = poseI[0].shape[0]
         if self.predict_init_pose and self.train_init_pose:
             poses[0].append(poseI[0])
-            poses[1].append(poseI[1])
+            poses[1].append(poseI[1].reshape(B, 3))  # the predictors' translation is [B,3]
             if self.uncer_prop:
                 sig.append(torch.eye(6, dtype=poseI[0].dtype, device=poseI[0].device).repeat(poseI[0].shape[0], 1, 1))
         pose = poseI
@@ -229,7 +231,10 @@ class LeastSquareTracking(nn.Module):
                     sig.append(out[1])
             pose = out[0]
             poses[0].append(pose[0])
-            poses[1].append(pose[1])
+            poses[1].append(pose[1].reshape(B, 3))  # [B,3] after an update (geometry.py:122)
+        if self.uncer_prop and len(sig) != len(poses[0]):
+            raise NotImplementedError("uncer_prop needs the U_IC solver's JtWJ output (the IC tracker returns "
+                                      "none, algorithms.py:101)")
         pyr_R, pyr_t = torch.stack(poses[0], dim=1), torch.stack(poses[1], dim=1)
         return (pyr_R, pyr_t, torch.stack(sig, dim=1)) if self.uncer_prop else (pyr_R, pyr_t)
 

@@ -238,7 +238,7 @@ def inverse_update_pose(H, JtR, pose):
     dR = _twist2mat(-xi[:, :3])
     dt = -torch.bmm(dR, xi[:, 3:].reshape(B, 3, 1))
     R1, t1 = geometry.batch_Rt_compose(R.double(), t.double(), dR, dt)
-    return [R1.to(R.dtype), t1.to(t.dtype).view(B, 3, 1)]
+    return [R1.to(R.dtype), t1.to(t.dtype).view(B, 3)]  # t [B,3] as batch_Rt_compose returns it (geometry.py:122)
 
 
 class DirectSolverNet(nn.Module):
@@ -311,7 +311,7 @@ class DirectSolverNet(nn.Module):
         JtR_flat = JtR_s.permute(1, 2, 0).reshape(B, -1)  # [B, 6, S]: as the reference's cat(dim=2)
         damp = self.net(torch.cat((JtR_flat, JtJ.view(B, -1)), dim=1))
         R1, t1 = ic.damped_update(JtJ, JtR, damp.view(1, B, 6), pose)
-        return [R1[0], t1[0]]
+        return [R1[0], t1[0].view(B, 3)]
 
 
 # ------------------------------------------------------------------ init-pose networks
@@ -456,7 +456,7 @@ class TrustRegionBase(nn.Module):
         if TS.needs_torch_path(JtJ, JtR, *pose0):
             return TS.damped_update(JtJ, JtR, pose0)
         R, t = ic.damped_update(JtJ, JtR.reshape(B, 6), None, pose0)
-        return [R[0], t[0]]
+        return [R[0], t[0].view(B, 3)]  # inverse_update_pose's t [B,3] (geometry.py:122)
 
     def _weights(self, pose, x0, x1, invD0, invD1, K, wPrior, obj_mask0, obj_mask1):
         """(weights [B,1,H,W] of the learned estimator, residual map, occlusion) or Nones."""
@@ -488,7 +488,7 @@ class TrustRegionBase(nn.Module):
                 else:
                     R, t, _, _, _ = ic.iterate(pose, x0, x1, invD0, invD1, K, None, None, first=(it == 0),
                                                no_uncertainty=True, weights=w, obj_mask0=m0, obj_mask1=obj_mask1)
-                    pose = [R, t]
+                    pose = [R, t.view(B, 3)]  # the updated t is [B,3] (batch_Rt_compose, geometry.py:122)
         weights = w if w is not None else torch.ones((1, 1, 1, 1), dtype=x0.dtype, device=x0.device).expand(B, C, H, W)
         return pose, weights
 
@@ -596,7 +596,9 @@ class TrustRegionInverseWUncertainty(nn.Module):
                     status = torch.zeros(1, dtype=torch.int32, device=x0.device)
                 out = ic.solve_level(pose10, x0, x1, invD0, invD1, K, sigma0, sigma1, iters=self.max_iterations,
                                      return_jtj=self.uncer_prop, check=False, status=status, **kw)
-        pose = [out[0], out[1]]
+        # an updated translation is [B,3], as the reference's batch_Rt_compose returns it
+        # (geometry.py:122); with no iteration the initial pose passes through unchanged
+        pose = [out[0], out[1].view(B, 3)] if self.max_iterations > 0 else list(pose10)
         if self.combine_icp:
             weights = torch.full((1, 1, 1, 1), self._icp_scale(), dtype=x0.dtype, device=x0.device).expand(B, 1, H, W)
         else:
@@ -648,7 +650,7 @@ class TrustRegionInverseWUncertainty(nn.Module):
         if TS.needs_torch_path(JtJ, JtR, *pose0):
             return TS.damped_update(JtJ, JtR, pose0)
         R, t = ic.damped_update(JtJ, JtR.reshape(B, 6), None, pose0)
-        return [R[0], t[0]]
+        return [R[0], t[0].view(B, 3)]  # inverse_update_pose's t [B,3] (geometry.py:122)
 
     def compute_jtj(self, jac):
         """J [B,C,HW,6] -> JtJ [B,6,6] (algorithms.py:812-820)."""

@@ -31,7 +31,11 @@ def needs_torch_path(*tensors):
     """the PyTorch path takes CPU tensors, and calls with grad enabled where an
     input requires grad; device tensors at inference go to libdpft_ic.so."""
     ts = [t for t in tensors if isinstance(t, torch.Tensor)]
-    if not ts[0].is_cuda:
+    on_dev = [t.is_cuda for t in ts]
+    if any(on_dev) and not all(on_dev):
+        raise ValueError("the solver's tensors span devices (%s); move them to one device first"
+                         % ", ".join(sorted({str(t.device) for t in ts})))
+    if not on_dev[0]:
         return True
     return torch.is_grad_enabled() and any(t.requires_grad for t in ts)
 
@@ -126,7 +130,7 @@ def damped_update(JtJ, JtR, pose, diag_add=None):
         + (1 - torch.cos(th)).view(B, 1, 1) * torch.bmm(Kx, Kx)
     dt = -torch.bmm(dR, xi[:, 3:].reshape(B, 3, 1))
     R1, t1 = geometry.batch_Rt_compose(R.double(), t.double().reshape(B, 3, 1), dR, dt)
-    return [R1.to(R.dtype), t1.to(t.dtype).view(B, 3, 1)]
+    return [R1.to(R.dtype), t1.to(t.dtype).view(B, 3)]  # t [B,3]: batch_Rt_compose's t1.view(-1,3) (geometry.py:122)
 
 
 # ------------------------------------------------------------------ U_IC

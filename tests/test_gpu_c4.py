@@ -544,3 +544,54 @@ def test_grouped_solve_deterministic_and_graph_capturable():
         g.replay()
         torch.cuda.synchronize()
         assert torch.equal(R, Re) and torch.equal(t, te)
+
+
+@pytest.mark.gpu
+def test_nchw_solve_packs_on_entry_bit_identical():
+    """A solve handed the reference's NCHW features (C % 16 == 0, one sigma plane) packs them
+    once on entry into the workspace and runs the channel-quad kernels (dpft_ic_solve_level /
+    dpft_ic_solve_pyramid, packs_on_entry): the cfg3 batch at 640x480, C = 32 -- the pyramid
+    entry point, the per-level entry point and the drop-in solver module's forward
+    (algorithms.py:611-723) chained over the levels -- gives the poses of the pre-packed solve
+    bit for bit, and those lie on the reference's run of the batch."""
+    from deep_prob_feature_track_amd import ic
+    from deep_prob_feature_track_amd.models.algorithms import TrustRegionInverseWUncertainty
+    dev = _dev()
+    name = "cfg3_b8_640x480_c32"
+    case, z = golden_io.load(name)
+    lv = golden_io.levels_torch(case, torch.float32, dev)
+    K = torch.from_numpy(case["K"]).to(dev)
+    R0, t0 = golden_io.init_pose(case, torch.float32, dev)
+    B, C, H, W = lv[0]["f0"].shape
+    assert C % 16 == 0
+
+    def levels(pack):
+        return [dict(x0=ic.pack_features(d["f0"]) if pack else d["f0"], x1=ic.pack_features(d["f1"]) if pack else d["f1"],
+                     invD0=d["invD0"], invD1=d["invD1"], sigma0=d["s0"], sigma1=d["s1"]) for d in lv]
+    outs = {}
+    for pack in (True, False):
+        solver = ic.PyramidSolver(levels(pack), K, iters=3, remove_tru_sigma=True)
+        for per_level in (False, True):
+            R, t = R0.clone().contiguous(), t0.reshape(B, 3).clone().contiguous()
+            solver.run(R, t, per_level=per_level)
+            torch.cuda.synchronize()
+            ic.check_status(solver.status)
+            outs[(pack, per_level)] = (R, t)
+    for key in outs:
+        assert torch.equal(outs[key][0], outs[(True, False)][0]) and torch.equal(outs[key][1], outs[(True, False)][1]), key
+    # the module, level by level (LeastSquareTracking.forward's loop) on NCHW and packed features
+    tr = TrustRegionInverseWUncertainty(3, remove_tru_sigma=True)
+    mods = {}
+    for pack in (True, False):
+        pose = [R0.clone(), t0.reshape(B, 3, 1).clone()]
+        with torch.no_grad():
+            for l, d in reversed(list(enumerate(levels(pack)))):
+                pose = tr(pose, d["x0"], d["x1"], d["invD0"], d["invD1"], K / 2 ** l, d["sigma0"].expand(B, C, -1, -1),
+                          d["sigma1"].expand(B, C, -1, -1), vis_res=False)[0]
+        mods[pack] = pose
+    assert torch.equal(mods[True][0], mods[False][0]) and torch.equal(mods[True][1], mods[False][1])
+    assert mods[False][1].shape == (B, 3)
+    dev_pose = golden_io.pose_deviation(mods[False][0], mods[False][1], z, "f32")
+    floor = golden_io.noise_floor(z)
+    bound = np.maximum(SE3_TOL, 1.5 * floor[-1]) if floor is not None else SE3_TOL
+    assert (dev_pose <= bound).all(), (dev_pose, bound)

@@ -350,12 +350,12 @@ def test_damped_update_matches_fp64_reference_update():
              1e-6 * torch.diagonal(JtJ.double(), dim1=1, dim2=2).sum(1).view(B, 1, 1) * eye)
         Rr, tr = inverse_update_pose(H, JtR.double(), [R.double(), t.double()])
         assert (Rs[s].cpu().double() - Rr).abs().max().item() < 2e-6
-        assert (ts[s].cpu().double() - tr).abs().max().item() < 2e-6
+        assert (ts[s].cpu().double().view(B, 3) - tr).abs().max().item() < 2e-6
     # S = 1 without extra damping: lev_mar_H's matrix
     R1, t1 = ic.damped_update(JtJ.to(dev), JtR.to(dev), None, [R.to(dev), t.to(dev)])
     H = JtJ.double() + 1e-6 * torch.diagonal(JtJ.double(), dim1=1, dim2=2).sum(1).view(B, 1, 1) * eye
     Rr, tr = inverse_update_pose(H, JtR.double(), [R.double(), t.double()])
-    assert (R1[0].cpu().double() - Rr).abs().max().item() < 2e-6 and (t1[0].cpu().double() - tr).abs().max() < 2e-6
+    assert (R1[0].cpu().double() - Rr).abs().max().item() < 2e-6 and (t1[0].cpu().double().view(B, 3) - tr).abs().max() < 2e-6
 
 
 def test_iterate_poses_equals_per_pose_iterate():
@@ -473,5 +473,6 @@ def test_gn_solver_and_ic_precompute_jacobian_match_oracle():
     R_ref, t_ref, _ = O.damped_solve_update(JtJ, JtR, dd(R0), dd(t0).view(B, 3, 1))
     for mod in (TrustRegionInverseWUncertainty(), TrustRegionBase()):
         R, t = mod.GN_solver(g(JtJ.float()), g(JtR.float()), [g(R0), g(t0)])
+        assert t.shape == (B, 3)  # inverse_update_pose's translation layout (geometry.py:122)
         assert (R.cpu().double() - R_ref).abs().max().item() < 2e-6
         assert (t.cpu().double().view(B, 3, 1) - t_ref).abs().max().item() < 2e-6

@@ -110,7 +110,8 @@ def test_cpu_module_forward_matches_reference(name):
         R, t = m(T["img0"], T["img1"], T["depth0"], T["depth1"], T["K"], **kw)
         B = R.shape[0]
         assert np.abs(R.numpy() - z["R"]).max() < 1e-4
-        assert np.abs(t.numpy().reshape(B, 3) - z["t"].reshape(B, 3)).max() < 1e-4
+        assert t.shape == z["t"].shape, (t.shape, z["t"].shape)  # the reference's [B,3] translation
+        assert np.abs(t.numpy() - z["t"]).max() < 1e-4
         _, loss = m.compute_residual(T["img0"], T["img1"], T["depth0"], T["depth1"], T["K"],
                                      poseI=[torch.from_numpy(z["R"]), torch.from_numpy(z["t"])], level_i=0, **kw)
         np.testing.assert_allclose(loss.numpy(), z["res_pose_loss"], rtol=1e-4)
@@ -263,14 +264,57 @@ def test_gradients_flow_through_the_solve():
         assert g is not None and torch.isfinite(g).all() and g.abs().max() > 0
 
 
-def test_training_mode_forward_returns_stacked_level_poses():
-    """Training mode (LeastSquareTracking.py:568-575): per-level poses [B,4,3,3] / [B,4,3,1]
-    (levels 3 .. 0), the last one the tracked pose; a loss on them reaches the encoder."""
-    m, T = _loaded("convrgbd2_c8")
-    m.train()
-    R, t = m(T["img0"], T["img1"], T["depth0"], T["depth1"], T["K"])
+def _loaded_opts(name, **extra):
+    spec = G.MODEL_CASES[name]
+    opts = dict(spec["opts"], **extra)
+    m = LeastSquareTracking(spec["encoder"], spec["uncertainty"], 3, spec.get("mest", "None"),
+                            spec.get("solver", "Direct-Nodamping"), options=default_options(**opts),
+                            **spec.get("ctor", {}))
+    m.load_state_dict({k: torch.from_numpy(recipe.synthetic_weights(k, v.shape)) for k, v in m.state_dict().items()})
+    inp = G.model_inputs(spec["pairs"], spec["masks"])
+    return m, {k: torch.from_numpy(v) for k, v in inp.items()}
+
+
+@pytest.mark.parametrize("name,extra", [
+    ("convrgbd2_c8", {}),
+    ("convrgbd2_c8", {"train_uncer_prop": True}),
+    ("convrgbd_c16_sfm", {"train_init_pose": True}),
+    ("convrgbd_c16_sfm", {"train_init_pose": True, "train_uncer_prop": True}),
+    ("rgb_ic_mest2w", {}),
+])
+def test_training_mode_forward_returns_stacked_level_poses(name, extra):
+    """Training mode (LeastSquareTracking.py:568-575): per-level poses R [B,L,3,3], t [B,L,3] --
+    the reference's translation layout (batch_Rt_compose returns t.view(-1,3), geometry.py:122;
+    its criterions index t_est[:, idx] as [B,3]) -- with L = 4 levels 3 .. 0, or 5 with a trained
+    init pose (its pose first, LeastSquareTracking.py:336-343), sigma_ksi [B,L,6,6] with
+    uncer_prop (the JtWJ of each level, the identity for the init pose).  The stacked level-0
+    pose equals the eval-mode forward on the same inputs (batchnorm frozen in both), and a loss
+    on it reaches the encoder."""
+    m, T = _loaded_opts(name, **extra)
     B = T["img0"].shape[0]
-    assert R.shape == (B, 4, 3, 3) and t.shape == (B, 4, 3, 1)
+    with torch.no_grad():
+        m.eval()
+        R_ev, t_ev = m(T["img0"], T["img1"], T["depth0"], T["depth1"], T["K"])
+    m.train()
+    for mod in m.modules():  # batch statistics would change the features; compare like with like
+        if isinstance(mod, torch.nn.modules.batchnorm._BatchNorm):
+            mod.eval()
+    out = m(T["img0"], T["img1"], T["depth0"], T["depth1"], T["K"])
+    L = 5 if extra.get("train_init_pose") else 4
+    R, t = out[0], out[1]
+    assert R.shape == (B, L, 3, 3) and t.shape == (B, L, 3)
+    if extra.get("train_uncer_prop"):
+        assert len(out) == 3 and out[2].shape == (B, L, 6, 6)
+        if L == 5:
+            assert torch.equal(out[2][:, 0], torch.eye(6).expand(B, 6, 6))
+        assert torch.isfinite(out[2]).all()
+    else:
+        assert len(out) == 2
+    assert torch.allclose(R[:, -1].detach(), R_ev, atol=1e-5) and torch.allclose(t[:, -1].detach(), t_ev, atol=1e-5)
     (R[:, -1].sum() + t[:, -1].sum()).backward()
-    grads = [p.grad for p in m.encoder.parameters() if p.grad is not None]
-    assert grads and all(torch.isfinite(g).all() for g in grads) and any(g.abs().max() > 0 for g in grads)
+    grads = [p.grad for p in m.encoder.parameters() if p.grad is not None] if m.encoder is not None else []
+    if m.encoder is not None:
+        assert grads and all(torch.isfinite(g).all() for g in grads) and any(g.abs().max() > 0 for g in grads)
+    if extra.get("train_init_pose"):
+        pg = [p.grad for p in m.pose_predictor.parameters() if p.grad is not None]
+        assert pg and any(g.abs().max() > 0 for g in pg)
