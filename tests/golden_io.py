@@ -106,6 +106,52 @@ def loo_exceedances(z, i=-1, factor=1.5, tol=1e-4, prec="f32"):
     return out
 
 
+# ---- the chained-trajectory parity rule, frozen in round 6 -------------------
+# Changing one of these is a change of the contract, not a calibration after a red run:
+# tests/test_parity_rule.py pins every value and the rule's behaviour on synthetic data.
+SE3_TOL = 1e-4        # north_star: 1e-4 on the estimated se(3) (R and t entries)
+FLOOR_FACTOR = 1.5    # a pair's bound: max(SE3_TOL, FLOOR_FACTOR x that pair's OWN noise floor)
+NOISE_RUNS = 33       # rounding-only reference runs behind every floor (32 jittered + the 1-thread run)
+EXCEEDANCE_CAP = 4    # at most this many pairs per iteration beyond their own bound ...
+EXCEEDANCE_SCALE = 2  # ... each within EXCEEDANCE_SCALE x its OWN bound (never the batch's floor)
+
+
+def allowance(z, i=-1):
+    """Pairs that may exceed their own bound at iteration i: as many as ONE of the reference's
+    own rounding-only runs exceeds against the other runs' floors (loo_exceedances), capped at
+    EXCEEDANCE_CAP."""
+    return min(loo_exceedances(z, i, FLOOR_FACTOR, SE3_TOL), EXCEEDANCE_CAP)
+
+
+def envelope(dev, z, i=-1):
+    """The frozen rule for chained poses at iteration i (dev = per-pair max(|dR|, |dt|) against
+    the fixture's fp32 run, [B]) -> (violations [str], bound [B] per pair, floor [B], over [pairs
+    beyond their own bound]).  Per pair: dev <= max(SE3_TOL, FLOOR_FACTOR x own floor); at most
+    allowance(z, i) pairs beyond that, each within EXCEEDANCE_SCALE x its own bound; and no more
+    pairs beyond SE3_TOL than the most any rounding-only run of the reference moves that far.
+    `bound` comes back with the admitted pairs' ceiling in place (for the fp64 comparison)."""
+    floor = noise_floor(z)[i]
+    bound = np.maximum(SE3_TOL, FLOOR_FACTOR * floor)
+    over = np.flatnonzero(dev > bound)
+    allowed = allowance(z, i)
+    msgs = []
+    detail = {int(b): (f"{dev[b]:.2e}", f"floor {floor[b]:.2e}") for b in over[:20]}
+    if over.size > allowed:
+        msgs.append(f"iter {i}: {over.size} pairs beyond max({SE3_TOL}, {FLOOR_FACTOR} x own floor), the rule "
+                    f"admits {allowed}: {detail}")
+    ceiling = EXCEEDANCE_SCALE * bound
+    bad = np.flatnonzero(dev > ceiling)
+    if bad.size:
+        msgs.append(f"iter {i}: beyond {EXCEEDANCE_SCALE} x their own bound: "
+                    + str({int(b): (f"{dev[b]:.2e}", f"bound {bound[b]:.2e}") for b in bad[:20]}))
+    n_over = int((dev > SE3_TOL).sum())
+    n_ref = noise_counts_beyond(z, SE3_TOL, i)
+    if n_over > int(n_ref.max()):
+        msgs.append(f"iter {i}: {n_over} pairs beyond {SE3_TOL} of the fp32 run; the reference's own rounding-only "
+                    f"runs move at most {int(n_ref.max())}")
+    return msgs, np.where(dev > bound, ceiling, bound), floor, over
+
+
 def noise_counts_beyond(z, tol, i=-1, prec="f32"):
     """Per rounding-only run, the number of pairs whose pose at iteration i moved by more
     than `tol` from the fixture's run [N] (how many pairs the reference itself moves by
