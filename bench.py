@@ -127,6 +127,7 @@ def l0_traffic(pairs, group, kernel, icp=False):
     for f in sorted(glob.glob(os.path.join(ROOT, "profiles", "*_l0_traffic.json")), reverse=True):
         d = json.load(open(f))
         if (d.get("level", 0) == 0 and d.get("pairs_per_launch", 8) == pairs and d.get("group", pairs) == group
+                and d.get("kbench_mode", "level") == "level"
                 and d.get("isa_sha256") == isa
                 and bool(d.get("combine_icp", False)) == icp and d.get("isa_sha256_icp") == isa_icp):
             return {"hbm_bytes": d["hbm_bytes"], "source": os.path.relpath(f, ROOT)}

@@ -28,6 +28,10 @@ p.add_argument("--width", type=int, default=640,
 p.add_argument("--icp", action="store_true", help="cfg5: with the combine_ICP term (bench.py --icp)")
 p.add_argument("--from-solve", action="store_true",
                help="start from the poses of one full pyramid solve (the bench's operating point) instead of identity")
+p.add_argument("--save-poses", default=None, help="write the start poses (after --from-solve) to this .pt file")
+p.add_argument("--load-poses", default=None,
+               help="start from poses saved by --save-poses (a variant library whose solve is not valid, e.g. "
+                    "tools/mk_loads_variant.py, replays the shipped solve's operating point)")
 a = p.parse_args()
 dev = torch.device("cuda:0")
 sel, levels, K = bench.make_batches(a.batch, 0, a.groups, dev, a.icp)
@@ -45,6 +49,12 @@ from deep_prob_feature_track_amd import _native as N
 if a.from_solve:
     solver.run(R, t)
     torch.cuda.synchronize()
+if a.load_poses:
+    saved = torch.load(a.load_poses, weights_only=True)
+    R.copy_(saved["R"].to(dev))
+    t.copy_(saved["t"].to(dev))
+if a.save_poses:
+    torch.save({"R": R.cpu(), "t": t.cpu()}, a.save_poses)
 solver.prepare_extrema()  # per-level sigma0 extrema slots (the levels run with EXTREMA_READY)
 for level in ([a.level] if a.level >= 0 else range(len(solver.calls))):
     c = solver.calls[level]

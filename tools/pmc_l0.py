@@ -40,10 +40,14 @@ def isa_sha(kernel=None):
     return (B.isa_hashes(os.path.abspath(lib)) if lib else json.load(open(B.ISA_OUT))).get(kernel or B.L0_KERNEL)
 
 
+MODE = {"mode": "level", "load_poses": None}  # --mode reduce: the records-only launches (tools/mk_loads_variant.py)
+
+
 def run_pass(counter, outdir, groups, icp=False, level=0):
+    start = ["--load-poses", os.path.abspath(MODE["load_poses"])] if MODE["load_poses"] else ["--from-solve"]
     cmd = ["timeout", "-s", "KILL", "90", "rocprofv3", "--pmc", counter, "--output-format", "csv", "-d", outdir,
            "-o", "c", "--", sys.executable, os.path.join(ROOT, "tools", "kbench.py"), "--c4", "--level", str(level),
-           "--mode", "level", "--from-solve", "--reps", "10", "--warm-ms", "0", "--groups", str(groups)] + (["--icp"] if icp else [])
+           "--mode", MODE["mode"], *start, "--reps", "10", "--warm-ms", "0", "--groups", str(groups)] + (["--icp"] if icp else [])
     env = dict(os.environ, TMPDIR="/tmp")
     if env.get("DPFT_LIB"):  # a variant library (tools/build_variants.py); the profiler runs from /tmp
         env["DPFT_LIB"] = os.path.abspath(env["DPFT_LIB"])
@@ -64,7 +68,8 @@ def parse(counter, outdir):
     # the last LEVEL0_LAUNCHES are kbench's level-0 launches (its first iteration + reps x 3);
     # before them, its --from-solve pyramid solve (marching launches per level depend on
     # the batch size: levels 1 and 0 at 8 pairs, every level at 128)
-    vals = [v for _, v in sorted(rows)[-LEVEL0_LAUNCHES:]]
+    n_last = 10 if MODE["mode"] == "reduce" else LEVEL0_LAUNCHES  # reduce: the 10 records-only launches
+    vals = [v for _, v in sorted(rows)[-n_last:]]
     if not vals:
         raise SystemExit(f"no ic_reduce_kernel rows for {counter}")
     if icp_rows:  # a level-0 iteration is the ICP pass + the reduce launch: their bytes together
@@ -81,7 +86,12 @@ def main():
     ap.add_argument("--level", type=int, default=0, help="pyramid level of the measured launches (traffic "
                     "of the coarser levels; only level 0 is matched by bench.py)")
     ap.add_argument("--from-dir", help="parse the fetch/ and write/ CSVs under this directory instead of running")
+    ap.add_argument("--mode", choices=["level", "reduce"], default="level",
+                    help="kbench mode: level (the solve's launch group, default; bench.py matches only this) or "
+                         "reduce (records-only launches, for variants whose solve is not valid)")
+    ap.add_argument("--load-poses", default=None, help="start poses saved by kbench --save-poses (with --mode reduce)")
     a = ap.parse_args()
+    MODE.update(mode=a.mode, load_poses=a.load_poses)
     tmp = os.path.join(ROOT, "gpurun_out", "pmc_l0")
     if a.from_dir:  # re-read the CSVs of an earlier run (same launch shape)
         fetch, nf = parse("FETCH_SIZE", os.path.join(a.from_dir, "fetch"))
@@ -94,7 +104,7 @@ def main():
     kernel = B.L0_KERNEL
     out = {"kernel": f"ic_reduce_kernel<32,Cs=1,tru,U_IC,c4>{' + icp_records_kernel' if a.icp else ''} level {a.level}, {a.groups} x 8 pairs per launch, 640x480 "
                      "(tools/kbench.py --mode level --from-solve)",
-           "level": a.level, "pairs_per_launch": 8 * a.groups, "group": 8,
+           "level": a.level, "pairs_per_launch": 8 * a.groups, "group": 8, "kbench_mode": a.mode,
            "src_sha256": src_sha(), "isa_sha256": isa_sha(kernel), "combine_icp": a.icp,
            **({"isa_sha256_icp": isa_sha(B.ICP_KERNEL)} if a.icp else {}), "launches": {"fetch": nf, "write": nw},
            "FETCH_SIZE_KiB": fetch, "WRITE_SIZE_KiB": write,
