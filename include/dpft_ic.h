@@ -146,6 +146,10 @@ size_t dpft_workspace_size(const DpftLevelDesc* desc);
  * R [B,3,3] (row-major) and t [B,3] are read and updated in place (fp32).
  * jtj_out [B,36] / jtr_out [B,6] (nullable) receive the LAST iteration's
  * undamped JtJ / JtR (the reference's `inv_sigma_ksi`, algorithms.py:716-721).
+ * NCHW features (no DPFT_FEATURES_C4) with C % 16 == 0, one sigma plane (or
+ * DPFT_NO_UNCERTAINTY) and iters >= 2 are packed once on entry into the workspace
+ * (dpft_workspace_size counts the two copies) and solved by the channel-quad kernels:
+ * the same poses, bit for bit, as a call handed the packed features.
  */
 int dpft_ic_solve_level(const DpftLevelDesc* desc, const DpftLevelTensors* tensors,
                         float* R, float* t, float* jtj_out, float* jtr_out,
