@@ -13,7 +13,7 @@ root=${GRAFT_REPO_ROOT:-$(cd "$(dirname "$0")/.." && pwd)}
 cd "$root"
 export TMPDIR=/tmp
 mkdir -p gpurun_out
-bench_extra=""
+bench_extra="--no-cpu-baseline"  # (the kernel profile; bench.py's own line carries the CPU baseline)
 [ -n "$icp" ] && bench_extra="--icp --no-cpu-baseline --no-compare"
 ( cd /tmp && timeout -k 10 240 rocprofv3 --kernel-trace --stats --output-format csv -d "$root/gpurun_out/${tag}_prof" \
     -o bench -- python3 "$root/bench.py" --steps 100 --warmup 10 $bench_extra ) > "gpurun_out/${tag}_prof.log" 2>&1
