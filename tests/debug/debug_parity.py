@@ -1,6 +1,6 @@
 """Debug helper: compare one HIP iteration with the oracle on a golden case (GPU box)."""
 import sys, os
-ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 sys.path[:0] = [ROOT, os.path.join(ROOT, "tests"), os.path.join(ROOT, "tests", "golden")]
 import numpy as np, torch
 import golden_io

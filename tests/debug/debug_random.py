@@ -1,6 +1,6 @@
 """Debug helper: one random case, HIP vs fp32 / fp64 oracle (GPU box)."""
 import sys, os
-ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 sys.path[:0] = [ROOT, os.path.join(ROOT, "tests"), os.path.join(ROOT, "tests", "golden")]
 import torch
 from oracle import ic_oracle as O

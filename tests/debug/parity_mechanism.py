@@ -15,7 +15,7 @@ jump (deviation > 10x the one-step deviation) and whether the extremum set diffe
 pixel of that pair (a direct flip) or elsewhere (the pair then moves through the coupled
 iterations that follow).
 
-  python tools/parity_mechanism.py [--dump gpurun_out/parity_dump.npz] [--out DESIGN-ready json] NAME...
+  python tests/debug/parity_mechanism.py [--dump gpurun_out/parity_dump.npz] [--out DESIGN-ready json] NAME...
 """
 import argparse
 import json
@@ -25,10 +25,10 @@ import sys
 import numpy as np
 import torch
 
-ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 sys.path[:0] = [ROOT, os.path.join(ROOT, "tests"), os.path.join(ROOT, "tests", "golden")]
 import golden_io  # noqa: E402
-from oracle import ic_oracle as O  # noqa: E402  (analysis tool: the oracle is the checker here)
+from oracle import ic_oracle as O  # noqa: E402  (test infrastructure: the oracle is the checker here)
 
 
 def ulps(a, b):
