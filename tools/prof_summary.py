@@ -49,7 +49,9 @@ def main():
     # Level bookkeeping is per stream.
     streams = sorted({int(r.get("Stream_Id", 0) or 0) for r in rows})
     solo_stream = streams[0]
-    state = collections.defaultdict(lambda: {"level": None, "n_red": None, "cur": [], "solves": []})
+    # packed: the solve packs NCHW features to channel quads on entry (pack_c4 kernels: bench.py's
+    # other_layout leg); its channel-quad launches are listed apart from the headline's
+    state = collections.defaultdict(lambda: {"level": None, "n_red": None, "cur": [], "solves": [], "packed": False})
     groups = collections.defaultdict(list)
     for r in rows:
         sid = int(r.get("Stream_Id", 0) or 0)
@@ -59,7 +61,7 @@ def main():
         if name.startswith("minmax_levels") and not nrm_grids:
             # one sigma0 pre-pass for all levels opens a solve; levels then advance every
             # ITERS reduce launches (extra level-0 launches after the solve stay level 0)
-            st["level"], st["n_red"] = top, 0
+            st["level"], st["n_red"], st["packed"] = top, 0, False
             if st["cur"]:
                 st["solves"].append(st["cur"])
                 st["cur"] = []
@@ -88,10 +90,12 @@ def main():
         elif st["n_red"] is not None and st["level"] is not None and name.startswith(("ic_reduce", "ic_split")):
             st["level"] = max(top - st["n_red"] // ITERS, 0)
             st["n_red"] += 1
+        if name.startswith("pack_c4"):
+            st["packed"] = True
         level = st["level"]
         if level is None:
             continue
-        layout = "nchw" if name.endswith("false>") else "c4"
+        layout = "nchw" if name.endswith("false>") else ("nchw packed on entry" if st["packed"] else "c4")
         mode = "solo" if sid == solo_stream else "side streams"
         if name.startswith(("ic_reduce", "ic_split", "finalize", "minmax", "icp_normals", "icp_records")):
             groups[(mode, layout if not name.startswith(("finalize", "minmax", "icp_normals", "icp_records")) else "-",
@@ -103,7 +107,8 @@ def main():
             st["solves"].append(st["cur"])
     # one channel-quad solve with nothing else in flight: the last solo one
     solves = state[solo_stream]["solves"]
-    c4 = [s for s in solves if any(n.endswith("true>") or n.startswith("ic_split") for _, _, _, n, _ in s)]
+    c4 = [s for s in solves if any(n.endswith("true>") or n.startswith("ic_split") for _, _, _, n, _ in s)
+          and not any(n.startswith("pack_c4") for _, _, _, n, _ in s)]
     one = c4[-1] if c4 else []
     # cut after the level-0 iterations of the solve (bench.py times extra level-0 launches after it)
     n0, cut = 0, len(one)
