@@ -508,7 +508,7 @@ def test_grouped_batches_solve_as_separate_calls(G):
         # fp32 noise floor at 640x480 is 9.7e-5)
         torch.testing.assert_close(R[sl(g)], Ra, rtol=0, atol=5e-5)
         torch.testing.assert_close(t[sl(g)], ta, rtol=0, atol=5e-5)
-        for level in (0, 2):  # marching and split schedules
+        for level in (0, 1, 2):  # marching (level 1: the grid + pool split against the 8-pair grid) and split
             assert np.array_equal(_invalid_counts(grouped, level, R, t)[sl(g)],
                                   _invalid_counts(alone, level, R[sl(g)], t[sl(g)]))
     one_batch = ic.PyramidSolver(levels, K, iters=3, remove_tru_sigma=True)

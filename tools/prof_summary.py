@@ -17,6 +17,12 @@ import json
 import re
 
 
+def is_c4(name):
+    """ic_reduce_kernel<CT, CS1, TRU, MODE, C4[, FOLD]>: the channel-quad layout's instances"""
+    m = re.match(r"ic_reduce_kernel<([^>]*)>", name)
+    return bool(m) and m.group(1).split(", ")[4] == "true"
+
+
 def short(name):
     n = name.replace("(anonymous namespace)::", "").replace("void ", "")
     m = re.match(r"([A-Za-z_0-9]+(<[^>]*>)?)", n)
@@ -95,7 +101,8 @@ def main():
         level = st["level"]
         if level is None:
             continue
-        layout = "nchw" if name.endswith("false>") else ("nchw packed on entry" if st["packed"] else "c4")
+        layout = ("nchw packed on entry" if st["packed"] else "c4") if (is_c4(name) or not name.startswith("ic_reduce")) \
+            else "nchw"
         mode = "solo" if sid == solo_stream else "side streams"
         if name.startswith(("ic_reduce", "ic_split", "finalize", "minmax", "icp_normals", "icp_records")):
             groups[(mode, layout if not name.startswith(("finalize", "minmax", "icp_normals", "icp_records")) else "-",
@@ -107,7 +114,7 @@ def main():
             st["solves"].append(st["cur"])
     # one channel-quad solve with nothing else in flight: the last solo one
     solves = state[solo_stream]["solves"]
-    c4 = [s for s in solves if any(n.endswith("true>") or n.startswith("ic_split") for _, _, _, n, _ in s)
+    c4 = [s for s in solves if any(is_c4(n) or n.startswith("ic_split") for _, _, _, n, _ in s)
           and not any(n.startswith("pack_c4") for _, _, _, n, _ in s)]
     one = c4[-1] if c4 else []
     # cut after the level-0 iterations of the solve (bench.py times extra level-0 launches after it)
