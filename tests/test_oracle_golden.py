@@ -19,6 +19,18 @@ CASES = list(recipe.CASES)
 SLOW_F64 = {"cfg3_b8_640x480_c32", "cfg3_b8q2_640x480_c32", "cfg3_b8q7_640x480_c32",  # ~35 s per fp64 run
             "cfg4_sweep256_160x120_c8", "cfg4_sweep256_rotx10_160x120_c8", "cfg4_sweep256_tz10_160x120_c8",
             "cfg4_sweep256_ry011_160x120_c8", "cfg4_sweep256_tz012_160x120_c8"}
+# The CPU suite stays within a few minutes: of the large-batch fixtures (20-60 s of oracle work
+# each in fp32), cfg3_b8 and cfg4_sweep256 pin the oracle by default; the other six -- more
+# batches of the same two configurations, whose GPU parity tests run against the reference
+# fixtures directly -- with DPFT_ORACLE_ALL=1 (≈ 6 more minutes on 8 CPUs).
+OPT_IN = {"cfg3_b8q2_640x480_c32", "cfg3_b8q7_640x480_c32", "cfg4_sweep256_rotx10_160x120_c8",
+          "cfg4_sweep256_tz10_160x120_c8", "cfg4_sweep256_ry011_160x120_c8", "cfg4_sweep256_tz012_160x120_c8"}
+
+
+def _skip_opt_in(name):
+    import os
+    if name in OPT_IN and not os.environ.get("DPFT_ORACLE_ALL"):
+        pytest.skip("another batch of cfg3 / cfg4 (DPFT_ORACLE_ALL=1 runs it; the GPU tests use it directly)")
 
 
 def run_oracle(name, dtype):
@@ -50,6 +62,7 @@ def test_oracle_matches_reference(name, prec):
     dtype = torch.float64 if prec == "f64" else torch.float32
     if name in SLOW_F64 and prec == "f64":
         pytest.skip("a large batch in fp64: the fp64 oracle is pinned by the other cases")
+    _skip_opt_in(name)
     if f"{prec}_R" not in golden_io.load(name, check_digests=False)[1]:
         pytest.skip(f"reference cannot run {prec} for {name}")
     case, z, trace = run_oracle(name, dtype)
@@ -130,6 +143,7 @@ def test_oracle_restarted_iterations_exact(name, prec):
     dtype = torch.float64 if prec == "f64" else torch.float32
     if name in SLOW_F64 and prec == "f64":
         pytest.skip("8 pairs at 640x480 in fp64: the fp64 oracle is pinned by the other cases")
+    _skip_opt_in(name)
     case, z = golden_io.load(name)
     if f"{prec}_R" not in z:
         pytest.skip(f"reference cannot run {prec} for {name}")
