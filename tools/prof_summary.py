@@ -77,6 +77,8 @@ def main():
             # per level) and the sigma0 pre-pass leave the level alone
             st["level"] = nrm_grids.index(int(r["Grid_Size_X"]))
             st["n_red"] = None
+            if st["level"] == top:
+                st["packed"] = False
             if st["level"] == top and st["cur"]:
                 st["solves"].append(st["cur"])
                 st["cur"] = []
@@ -96,7 +98,7 @@ def main():
         elif st["n_red"] is not None and st["level"] is not None and name.startswith(("ic_reduce", "ic_split")):
             st["level"] = max(top - st["n_red"] // ITERS, 0)
             st["n_red"] += 1
-        if name.startswith("pack_c4"):
+        if name.startswith(("pack_c4_x4", "pack_c4_pair")):  # (pack_c4_kernel: the bench's own input packing)
             st["packed"] = True
         level = st["level"]
         if level is None:
@@ -115,7 +117,7 @@ def main():
     # one channel-quad solve with nothing else in flight: the last solo one
     solves = state[solo_stream]["solves"]
     c4 = [s for s in solves if any(is_c4(n) or n.startswith("ic_split") for _, _, _, n, _ in s)
-          and not any(n.startswith("pack_c4") for _, _, _, n, _ in s)]
+          and not any(n.startswith(("pack_c4_x4", "pack_c4_pair")) for _, _, _, n, _ in s)]
     one = c4[-1] if c4 else []
     # cut after the level-0 iterations of the solve (bench.py times extra level-0 launches after it)
     n0, cut = 0, len(one)
