@@ -48,8 +48,10 @@ def parse():
                    help="> 0: weak scaling instead, this many pairs per GPU per step")
     p.add_argument("--batch", type=int, default=8,
                    help="pairs per independent batch (one reference call: its own batch-global extrema)")
-    p.add_argument("--inflight", type=int, default=2,
-                   help="calls of the stream in flight per GPU (one stream, graph, workspace each)")
+    p.add_argument("--inflight", type=int, default=0,
+                   help="calls of the stream in flight per GPU (one stream, graph, workspace each; 0: 2, "
+                        "with --icp 4 -- the combine_ICP pass's latency-bound launches overlap the other "
+                        "calls' reduce launches, measured +1.5-3.5 %% against 2, DESIGN.md 4.4)")
     p.add_argument("--stream-group", type=int, default=0,
                    help="global batches of the stream per grouped call on each rank (0: enough for "
                         "--min-launch-pairs pairs per call)")
@@ -306,7 +308,7 @@ def main():
         _native.LIB_PATH = os.path.abspath(os.environ["DPFT_LIB"])
     from deep_prob_feature_track_amd import build as Bd, ic, shard
 
-    S = max(1, a.inflight)
+    S = max(1, a.inflight if a.inflight > 0 else (4 if a.icp else 2))
     weak = a.pairs_per_gpu > 0
     if weak:
         n_r = a.pairs_per_gpu
