@@ -61,3 +61,23 @@ def test_group_descriptor_validation_without_device_work():
     assert ws(32, N.REMOVE_TRU_SIGMA | N.COMBINE_ICP | G(8)) > 0           # ICP: per-batch depth extrema
     assert ws(2048, base | G(256)) > 0 and ws(2048, base | G(256)) == ws(2048, base)  # 8 batches of 256
     assert ws(2048, base | G(1024)) > 0
+
+
+def test_nchw_workspace_counts_the_entry_packs():
+    """dpft_workspace_size for NCHW features that dpft_ic_solve_level / _pyramid pack to channel
+    quads on entry (C % 16 == 0, one sigma plane, >= 2 iterations; include/dpft_ic.h): the
+    channel-quad workspace plus two packed feature planes, each B C H W floats rounded up to 256
+    bytes; where the solve does not pack (per-channel sigma, one iteration) nothing is added."""
+    import ctypes
+    L = N.lib()
+
+    def ws(B, C, Cs, H, W, iters, flags):
+        return L.dpft_workspace_size(ctypes.byref(N.LevelDesc(B, C, Cs, H, W, iters, flags, 0.0)))
+    rnd = lambda n: (n + 255) // 256 * 256
+    for B, C, H, W in ((8, 32, 480, 640), (1, 16, 120, 160), (3, 32, 61, 79)):
+        c4 = ws(B, C, 1, H, W, 3, N.REMOVE_TRU_SIGMA | N.FEATURES_C4)
+        nchw = ws(B, C, 1, H, W, 3, N.REMOVE_TRU_SIGMA)
+        assert c4 > 0 and nchw == c4 + 2 * rnd(B * C * H * W * 4), (B, C, H, W)
+    assert 0 < ws(2, 8, 1, 120, 160, 3, 0) == ws(2, 8, 1, 120, 160, 3, N.FEATURES_C4)   # C % 16 != 0: no pack
+    assert 0 < ws(2, 32, 1, 120, 160, 1, 0) == ws(2, 32, 1, 120, 160, 1, N.FEATURES_C4)  # one iteration: no pack
+    assert 0 < ws(2, 32, 32, 120, 160, 3, 0)  # per-channel sigma: the NCHW kernels, no pack
