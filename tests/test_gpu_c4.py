@@ -595,3 +595,32 @@ def test_nchw_solve_packs_on_entry_bit_identical():
     floor = golden_io.noise_floor(z)
     bound = np.maximum(SE3_TOL, 1.5 * floor[-1]) if floor is not None else SE3_TOL
     assert (dev_pose <= bound).all(), (dev_pose, bound)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("case", ["ragged", "misaligned"])
+def test_nchw_entry_pack_fallback_bit_identical(case):
+    """The entry pack's general kernel (pack_c4_pair_kernel: H W not a multiple of 4, or feature
+    pointers not 16-byte aligned -- a view at a one-float offset) gives the poses of the
+    caller-packed solve bit for bit (C = 16, so the NCHW solve packs on entry)."""
+    from deep_prob_feature_track_amd import ic
+    dev = _dev()
+    g = torch.Generator().manual_seed(11)
+    B, C, (H, W) = 3, 16, ((37, 70) if case == "ragged" else (40, 64))
+    f0 = torch.rand(B, C, H, W, generator=g)
+    f1 = torch.roll(f0, shifts=(1, 2), dims=(2, 3)) + 0.01 * torch.rand(B, C, H, W, generator=g)
+    s0 = 0.5 + torch.rand(B, 1, H, W, generator=g)
+    s1 = 0.5 + torch.rand(B, 1, H, W, generator=g)
+    d0 = 0.2 + torch.rand(B, 1, H, W, generator=g)
+    d1 = 0.2 + torch.rand(B, 1, H, W, generator=g)
+    K = torch.tensor([[W * 0.8, W * 0.8, (W - 1) / 2, (H - 1) / 2]]).repeat(B, 1)
+    f0, f1, s0, s1, d0, d1, K = (v.to(dev) for v in (f0, f1, s0, s1, d0, d1, K))
+    if case == "misaligned":  # the same values at a 4-byte offset from a 16-byte boundary
+        f0 = torch.cat([torch.zeros(1, device=dev), f0.reshape(-1)])[1:].view(B, C, H, W)
+        f1 = torch.cat([torch.zeros(1, device=dev), f1.reshape(-1)])[1:].view(B, C, H, W)
+        assert f0.data_ptr() % 16 and f1.data_ptr() % 16
+    pose = (torch.eye(3, device=dev).repeat(B, 1, 1), torch.zeros(B, 3, 1, device=dev))
+    ra = ic.solve_level(pose, f0, f1, d0, d1, K, s0, s1, iters=3, remove_tru_sigma=True)
+    rb = ic.solve_level(pose, f0, f1, d0, d1, K, s0, s1, iters=3, remove_tru_sigma=True, pack=True)
+    torch.cuda.synchronize()
+    assert torch.equal(ra[0], rb[0]) and torch.equal(ra[1], rb[1])
