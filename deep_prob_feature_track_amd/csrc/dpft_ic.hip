@@ -3505,6 +3505,7 @@ int pack_on_entry(const DpftLevelDesc& d, DpftLevelDesc& dc, DpftLevelTensors& t
   const long HW = (long)d.H * d.W, quads = (long)d.B * (d.C / 4);
   const bool x4 = HW % 4 == 0 && ((uintptr_t)tc.f0 % 16) == 0 && ((uintptr_t)tc.f1 % 16) == 0;
   const long n = x4 ? quads * (HW / 4) : quads * HW;
+  if ((n + kThreads - 1) / kThreads > 0x7fffffffL) return fail(DPFT_E_INVALID, "level too large to pack on entry");
   const dim3 grid((unsigned)((n + kThreads - 1) / kThreads), 2);
   if (x4)
     hipLaunchKernelGGL(pack_c4_x4_kernel, grid, dim3(kThreads), 0, st, tc.f0, tc.f1, p0, p1, n, HW / 4);
