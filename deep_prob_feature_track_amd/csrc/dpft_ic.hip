@@ -1094,6 +1094,13 @@ __device__ void block_minmax2(float& mn_a, float& mx_a, float& mn_b, float& mx_b
   mx_b = fmaxf(fmaxf(sm[3][0], sm[3][1]), fmaxf(sm[3][2], sm[3][3]));
 }
 
+// The pair record as pair_reduce2 stores it, kept in LDS too: a batch of one pair (q.group == 1)
+// is solved from it by the same workgroup, without the record's round trip through L2.
+__device__ __forceinline__ double* pair_rec_lds() {
+  __shared__ double rec[kPRec];
+  return rec;
+}
+
 // Run by the workgroup that completes the last pair: batch-global truncated-sigma
 // extrema over the pair records, corrections, then one thread per pair solves and
 // updates its pose (algorithms.py:2017-2103).
@@ -1167,6 +1174,23 @@ __device__ void finalize_batch(const FinParams& q) {
 // batch -- its own truncated-sigma extrema, as if it had been a call of its own.
 __device__ bool finalize_group(const FinParams& q, int b) {
   const int g = b / q.group, b0 = g * q.group;
+  if (q.group == 1) {  // a batch of one pair (B = 1): this workgroup, which reduced the pair, solves it
+    __syncthreads();     // from the pair record's LDS copy (pair_reduce2; the same values as stored)
+    FinParams qg = q;
+    qg.B = 1;
+    qg.R = q.R ? q.R + 9 * b : nullptr;
+    qg.t = q.t ? q.t + 3 * b : nullptr;
+    qg.jtj_out = q.jtj_out ? q.jtj_out + 36 * b : nullptr;
+    qg.jtr_out = q.jtr_out ? q.jtr_out + 6 * b : nullptr;
+    qg.invalid_out = q.invalid_out ? q.invalid_out + b : nullptr;
+    const double* lr = pair_rec_lds();
+    double r[46];
+    if (threadIdx.x == 0)
+#pragma unroll
+      for (int i = 0; i < 46; ++i) r[i] = lr[i];
+    finalize_batch_from(qg, [&](int, int i) { return r[i]; });
+    return true;
+  }
   if (!block_is_last(q.done_cnt + g, 1u, (uint32_t)q.group)) return false;
   FinParams qg = q;
   qg.B = q.group;
@@ -1302,17 +1326,22 @@ __device__ void pair_reduce2(const FinParams& q, int b, float* sc) {
   }
   __syncthreads();
   double* pr = q.prec + (size_t)b * kPRec;
+  double* lr = pair_rec_lds();
   if (tid < nf) {
     double v = 0.0;
     const float* col = L + tid * 65;
 #pragma unroll 16
     for (int r = 0; r < 64; ++r) v += (double)col[r];
-    st_ag(pr + (tid < 28 ? P_S + tid : tid < 35 ? P_CMN + (tid - 28) : P_CMX + (tid - 35)), v);
+    const int fld = tid < 28 ? P_S + tid : tid < 35 ? P_CMN + (tid - 28) : P_CMX + (tid - 35);
+    st_ag(pr + fld, v);
+    lr[fld] = v;
   } else if (tid >= 64 && tid < 64 + 2 * 7 && !tru) {
     st_ag(pr + P_CMN + (tid - 64), 0.0);  // (P_CMX follows P_CMN)
+    lr[P_CMN + (tid - 64)] = 0.0;
   } else if (tid >= 128 && tid < 132) {
-    const int i = tid - 128;
-    st_ag(pr + (i == 0 ? P_MN_ALL : i == 1 ? P_MN0 : i == 2 ? P_MX_ALL : P_MX0), (double)ex[i]);
+    const int i = tid - 128, fld = i == 0 ? P_MN_ALL : i == 1 ? P_MN0 : i == 2 ? P_MX_ALL : P_MX0;
+    st_ag(pr + fld, (double)ex[i]);
+    lr[fld] = (double)ex[i];
   }
 }
 
